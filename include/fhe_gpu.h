@@ -1,0 +1,180 @@
+/*
+ * fhe_gpu.h -- C ABI of the MI355X (gfx950) FHE polynomial-arithmetic
+ * backend (libfhe_gpu.so).  Drop-in replacement for the compute path of
+ * Digital-Defiance/node-fhe-accelerate: NTTProcessor, PolynomialRing,
+ * ModularArithmetic / BarrettReducer / MultiLimbModularArithmetic and
+ * BootstrapEngine::external_product, plus the N-API-visible
+ * ModularArithmetic class and detectHardware().
+ *
+ * Conventions
+ *   - Plain C: pointers + sizes, no C++ or torch types, no exceptions.
+ *   - Every function returns FHE_OK (0) or a negative FHE_ERR_* code; the
+ *     message (the reference's exception text where one exists) is
+ *     available from fhe_last_error() (thread-local).
+ *   - Polynomial data: contiguous row-major [batch][n] uint64 (the layout of
+ *     the reference's Polynomial / Metal buffers, metal_compute.mm:400-410).
+ *     Inputs may be any u64 and behave as x mod q (every reference path
+ *     reduces); outputs are canonical residues in [0, q).
+ *   - where = FHE_DEVICE: pointers are device (HBM) pointers of the context's
+ *     device, work is enqueued on the context stream and NOT synchronised.
+ *     where = FHE_HOST: pointers are host memory; the call stages through
+ *     device scratch and returns after the result is back in host memory.
+ *   - A context is immutable after creation (except its stream); concurrent
+ *     calls on distinct buffers are safe, as with the reference's shared
+ *     read-only NTTProcessor (encryption.cpp:520-533).
+ */
+#ifndef FHE_GPU_H
+#define FHE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FHE_GPU_ABI_VERSION 1
+
+/* ---- status codes (messages mirror the reference's std::invalid_argument) */
+#define FHE_OK 0
+#define FHE_ERR_DEGREE_POW2 (-1)     /* "Polynomial degree must be a power of 2"      ntt_processor.cpp:142 */
+#define FHE_ERR_DEGREE_RANGE (-2)    /* "Polynomial degree must be between 4 and 65536" ntt_processor.cpp:147 */
+#define FHE_ERR_MODULUS_EVEN (-3)    /* "Modulus must be odd"                          ntt_processor.cpp:152 */
+#define FHE_ERR_NOT_NTT_FRIENDLY (-4) /* "Modulus is not NTT-friendly: q != 1 (mod 2N)" ntt_processor.cpp:104 */
+#define FHE_ERR_COUNT (-5)           /* "Coefficient count must equal polynomial degree" ntt_processor.cpp:264 */
+#define FHE_ERR_NO_ROOT (-6)         /* "Could not find primitive root ..."            ntt_processor.cpp:127 */
+#define FHE_ERR_MONT_MODULUS (-7)    /* "Modulus must be odd and non-zero for Montgomery arithmetic" modular_arithmetic.cpp:54 */
+#define FHE_ERR_ZERO_MODULUS (-8)    /* "Modulus must be non-zero for Barrett reduction" modular_arithmetic.cpp:240 */
+#define FHE_ERR_INVALID_ARG (-9)
+#define FHE_ERR_UNSUPPORTED (-10)    /* parameter outside what the GPU kernels implement */
+#define FHE_ERR_DEVICE (-11)         /* HIP runtime error / no device */
+#define FHE_ERR_OOM (-12)
+
+#define FHE_MODE_COMPAT 0      /* the reference's transform, bit-exact */
+#define FHE_MODE_NEGACYCLIC 1  /* psi-twisted cyclic NTT: polymul == a*b mod (X^N+1) */
+
+#define FHE_HOST 0
+#define FHE_DEVICE 1
+
+typedef struct fhe_ctx fhe_ctx;
+
+/* Thread-local message of the last failing call on this thread. */
+const char *fhe_last_error(void);
+const char *fhe_version(void);
+
+/* ---- hardware ------------------------------------------------------------
+ * Replaces HardwareDetector::detect() (hardware_detector.mm; N-API
+ * detectHardware(), src/native/lib.rs:123-127, index.d.ts:22-30).          */
+typedef struct {
+    int32_t device_count;
+    int32_t compute_units;     /* of device 0 */
+    int32_t wavefront_size;
+    int32_t xcds;
+    uint64_t hbm_bytes;        /* of device 0 */
+    uint64_t lds_bytes_per_cu;
+    char arch[32];             /* "gfx950" */
+    char name[96];
+} fhe_hw_caps;
+int fhe_detect(fhe_hw_caps *caps);
+
+/* ---- context: NTTProcessor(degree, modulus) + PolynomialRing(degree, q)
+ * (ntt_processor.cpp:134-208, polynomial_ring.cpp:213-222).
+ * Validation order and messages follow the reference constructor.  n must
+ * be a power of two in [4, 65536]; the GPU kernels currently implement
+ * n <= 16384 and q < 2^62 (FHE_ERR_UNSUPPORTED otherwise).
+ * device: HIP device ordinal.                                              */
+int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out);
+void fhe_ctx_destroy(fhe_ctx *ctx);
+/* Use an existing hipStream_t (e.g. a torch stream) for FHE_DEVICE calls;
+ * NULL restores the context's own stream. */
+int fhe_ctx_set_stream(fhe_ctx *ctx, void *hip_stream);
+void *fhe_ctx_stream(const fhe_ctx *ctx);
+int fhe_ctx_synchronize(fhe_ctx *ctx);
+
+typedef struct {
+    uint32_t n, log_n;
+    uint64_t q;
+    uint64_t psi;          /* primitive 2N-th root (smallest generator rule, ntt_processor.cpp:92-128) */
+    uint64_t psi_inv;
+    uint64_t inv_n;        /* N^-1 mod q */
+    int32_t mode;
+    int32_t word_bits;     /* 32 (q < 2^30) or 64 (q < 2^62) kernel arithmetic */
+    int32_t device;
+    int32_t polys_per_block;
+    int32_t threads_per_block;
+} fhe_ctx_info;
+int fhe_ctx_get_info(const fhe_ctx *ctx, fhe_ctx_info *info);
+/* The reference's twiddle vectors psi^i / psi^-i, i < n (ntt_processor.cpp:188-202). */
+int fhe_ctx_get_twiddles(const fhe_ctx *ctx, uint64_t *forward, uint64_t *inverse);
+
+/* ---- transforms (ntt_processor.cpp:262-408) -----------------------------
+ * In place allowed (out == in).                                            */
+int fhe_ntt_fwd_batch(fhe_ctx *ctx, const uint64_t *in, uint64_t *out, size_t batch, int where);
+int fhe_ntt_inv_batch(fhe_ctx *ctx, const uint64_t *in, uint64_t *out, size_t batch, int where);
+/* out = to_ntt(a) (.) w, per polynomial (config C3: NTT + modmul). */
+int fhe_ntt_fwd_mul_batch(fhe_ctx *ctx, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch,
+                          int where);
+
+/* ---- PolynomialRing (polynomial_ring.cpp) ------------------------------- */
+/* multiply (:421-447) on coefficient-form inputs: inv(fwd(a) (.) fwd(b)). */
+int fhe_polymul_batch(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch, int where);
+/* pointwise_multiply (:493-530): c = a*b mod q over n*batch coefficients. */
+int fhe_pointwise_batch(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch, int where);
+int fhe_poly_add_batch(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch, int where);
+int fhe_poly_sub_batch(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch, int where);
+int fhe_poly_neg_batch(fhe_ctx *ctx, const uint64_t *a, uint64_t *c, size_t batch, int where);
+int fhe_poly_mul_scalar_batch(fhe_ctx *ctx, const uint64_t *a, uint64_t scalar, uint64_t *c, size_t batch,
+                              int where);
+
+/* ---- TFHE external product (bootstrap_engine.cpp:152-185, 431-518) ------
+ * glwe:  [batch][k+1][n] (k mask polynomials, then the body)
+ * ggsw:  [(k+1)*level rows][k+1][n], rows ordered as the reference's
+ *        ggsw.matrix (mask digit rows first, digit level inner).
+ * fhe_ggsw_prepare turns a coefficient-form GGSW into the NTT-domain form
+ * fhe_external_product_batch consumes (same shape).  k = 1 is implemented. */
+int fhe_ggsw_prepare(fhe_ctx *ctx, uint32_t k, uint32_t level, const uint64_t *ggsw, uint64_t *ggsw_ntt, int where);
+int fhe_external_product_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
+                               const uint64_t *ggsw_ntt, uint64_t *out, size_t batch, int where);
+/* decompose_polynomial (:152-185) for npoly polynomials: out [npoly][level][n]. */
+int fhe_decompose_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const uint64_t *poly, uint64_t *out,
+                        size_t npoly, int where);
+
+/* ---- context-free modular kernels --------------------------------------- */
+/* BarrettReducer::barrett_mul contract (modular_arithmetic.cpp:268-280):
+ * c[i] = a[i]*b[i] mod q for any u64 inputs, any q != 0. stream may be NULL. */
+int fhe_modmul_batch(uint64_t q, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t count, int where,
+                     int device, void *hip_stream);
+/* MultiLimbModularArithmetic (2 limbs, modular_arithmetic.cpp:471-625).
+ * q[2] little-endian limbs; a, b, c: count elements of 2 limbs each. */
+int fhe_ml_constants(const uint64_t q[2], uint64_t out[7]); /* q0,q1,r0,r1,r2_0,r2_1,q_inv */
+int fhe_ml_montmul_batch(const uint64_t q[2], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t count,
+                         int where, int device, void *hip_stream);
+
+/* ---- N-API ModularArithmetic class (index.d.ts:32-44, lib.rs:42-121) -----
+ * Scalar host functions with the reference's exact constants, including
+ * q_inv = -(q^-1 mod (2^64-1)) (modular_arithmetic.cpp:69).  consts[4] =
+ * {q, R mod q, R^2 mod q, q_inv}.                                            */
+int fhe_mont_constants_compat(uint64_t q, uint64_t consts[4]);
+uint64_t fhe_compat_montgomery_mul(const uint64_t consts[4], uint64_t a, uint64_t b);
+uint64_t fhe_compat_to_montgomery(const uint64_t consts[4], uint64_t a);
+uint64_t fhe_compat_from_montgomery(const uint64_t consts[4], uint64_t a);
+uint64_t fhe_compat_mod_add(uint64_t q, uint64_t a, uint64_t b);
+uint64_t fhe_compat_mod_sub(uint64_t q, uint64_t a, uint64_t b);
+
+/* ---- device memory helpers (for callers without their own allocator) --- */
+int fhe_dev_alloc(int device, size_t bytes, void **out);
+int fhe_dev_free(void *ptr);
+int fhe_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int fhe_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int fhe_device_synchronize(int device);
+
+/* Event timing on a stream (used by bench.py for HIP-event kernel timing). */
+int fhe_event_create(void **ev);
+int fhe_event_destroy(void *ev);
+int fhe_event_record(void *ev, void *hip_stream);
+int fhe_event_elapsed_ms(void *start, void *stop, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FHE_GPU_H */

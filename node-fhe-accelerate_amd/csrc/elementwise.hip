@@ -1,0 +1,262 @@
+// elementwise.hip -- HBM-streaming coefficient kernels.
+//
+//   modmul     : c = a*b mod q for any u64 a, b (BarrettReducer::barrett_mul
+//                contract, modular_arithmetic.cpp:268-280; Metal
+//                modmul_direct_batch, modmul_direct.metal:230-250;
+//                PolynomialRing::pointwise_multiply, polynomial_ring.cpp:493-530)
+//   add / sub  : ModularArithmetic::mod_add / mod_sub semantics
+//                (modular_arithmetic.cpp:122-153) elementwise
+//                (PolynomialRing::add/subtract, polynomial_ring.cpp:263-415)
+//   neg        : PolynomialRing::negate (polynomial_ring.cpp:340-355)
+//   mul_scalar : PolynomialRing::multiply_scalar (polynomial_ring.cpp:454-473)
+//   ml_montmul : MultiLimbModularArithmetic::montgomery_mul, 2 limbs
+//                (modular_arithmetic.cpp:525-625)
+//   decompose  : BootstrapEngine::decompose_polynomial (bootstrap_engine.cpp:152-185)
+//
+// All are HBM-bound: 16-byte (2 x u64) loads/stores per lane, grid-stride.
+#include "fhe_internal.hpp"
+
+namespace fhe {
+
+static constexpr int kBlock = 256;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+static inline size_t grid_for(size_t work) {
+    size_t g = (work + kBlock - 1) / kBlock;
+    const size_t cap = 256 * 16;  // 256 CUs x 16 blocks: grid-stride beyond
+    return g < 1 ? 1 : (g > cap ? cap : g);
+}
+
+__device__ __forceinline__ uint64_t red_any(uint64_t x, const ModConsts &m) {
+    return x < m.q ? x : mod64_slow(x, m.q, m.mu);
+}
+
+// (hi:lo) mod q by restoring shift-subtract; any q >= 1.  Slow path only.
+__device__ __noinline__ uint64_t mod128_slow(uint64_t hi, uint64_t lo, uint64_t q) {
+    uint64_t r = 0;
+    for (int i = 127; i >= 0; --i) {
+        const uint64_t bit = i >= 64 ? (hi >> (i - 64)) & 1 : (lo >> i) & 1;
+        const uint64_t c = r >> 63;
+        r = (r << 1) | bit;
+        if (c || r >= q) r -= q;
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint64_t mont64(uint64_t a, uint64_t b, uint64_t q, uint64_t qinv) {
+    const uint64_t lo = a * b, hi = __umul64hi(a, b);
+    const uint64_t m = lo * qinv;
+    return hi + __umul64hi(m, q) + (lo != 0);
+}
+
+__device__ __forceinline__ uint64_t modmul1(uint64_t a, uint64_t b, const ModConsts &m) {
+    if (m.fast) {
+        a = mod64_slow(a, m.q, m.mu);  // one Barrett step (q < 2^63)
+        b = mod64_slow(b, m.q, m.mu);
+        uint64_t t = mont64(a, b, m.q, m.qinv);  // a*b*R^-1 in [0, 2q)
+        t = mont64(t, m.r2, m.q, m.qinv);        // a*b       in [0, 2q)
+        return t >= m.q ? t - m.q : t;
+    }
+    return mod128_slow(__umul64hi(a, b), a * b, m.q);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_modmul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *__restrict__ c, size_t n,
+         ModConsts m) {
+    const size_t n2 = n / 2;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a) + i);
+        const u64x2 y = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(b) + i);
+        u64x2 z;
+        z.x = modmul1(x.x, y.x, m);
+        z.y = modmul1(x.y, y.y, m);
+        __builtin_nontemporal_store(z, reinterpret_cast<u64x2 *>(c) + i);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) c[n - 1] = modmul1(a[n - 1], b[n - 1], m);
+}
+
+__device__ __forceinline__ uint64_t addsub1(uint64_t x, uint64_t y, int sub, const ModConsts &m) {
+    x = red_any(x, m);
+    y = red_any(y, m);
+    if (sub) return x >= y ? x - y : m.q - (y - x);
+    const uint64_t s = x + y;
+    return (s < x || s >= m.q) ? s - m.q : s;
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_addsub(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *__restrict__ c, size_t n,
+         int sub, ModConsts m) {
+    const size_t n2 = n / 2;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a) + i);
+        const u64x2 y = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(b) + i);
+        u64x2 z;
+        z.x = addsub1(x.x, y.x, sub, m);
+        z.y = addsub1(x.y, y.y, sub, m);
+        __builtin_nontemporal_store(z, reinterpret_cast<u64x2 *>(c) + i);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) c[n - 1] = addsub1(a[n - 1], b[n - 1], sub, m);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_neg(const uint64_t *__restrict__ a, uint64_t *__restrict__ c, size_t n, uint64_t q) {
+    const size_t n2 = n / 2;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a) + i);
+        u64x2 z;
+        z.x = x.x == 0 ? 0 : q - x.x;
+        z.y = x.y == 0 ? 0 : q - x.y;
+        __builtin_nontemporal_store(z, reinterpret_cast<u64x2 *>(c) + i);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) c[n - 1] = a[n - 1] == 0 ? 0 : q - a[n - 1];
+}
+
+__device__ __forceinline__ uint64_t mulsc1(uint64_t x, uint64_t s, uint64_t sp, const ModConsts &m) {
+    if (m.q >> 63) return mod128_slow(__umul64hi(x, s), x * s, m.q);
+    const uint64_t r = x * s - __umul64hi(x, sp) * m.q;  // Shoup, [0, 2q)
+    return r >= m.q ? r - m.q : r;
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_mul_scalar(const uint64_t *__restrict__ a, uint64_t *__restrict__ c, size_t n, uint64_t s, uint64_t sp,
+             ModConsts m) {
+    const size_t n2 = n / 2;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a) + i);
+        u64x2 z;
+        z.x = mulsc1(x.x, s, sp, m);
+        z.y = mulsc1(x.y, s, sp, m);
+        __builtin_nontemporal_store(z, reinterpret_cast<u64x2 *>(c) + i);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) c[n - 1] = mulsc1(a[n - 1], s, sp, m);
+}
+
+// 2-limb Montgomery product exactly as MultiLimbModularArithmetic
+// (schoolbook mul_limbs, word-serial reduce with its bounded carry
+// propagation, one conditional subtraction).  c = [q0,q1,r0,r1,r2_0,r2_1,qinv]
+struct MLConsts { uint64_t q0, q1, qinv; };
+
+__device__ __forceinline__ void mac(uint64_t a, uint64_t b, uint64_t add, uint64_t &carry, uint64_t &out) {
+    // out = lo(a*b + add + carry), carry = hi(...)
+    const uint64_t lo = a * b, hi = __umul64hi(a, b);
+    uint64_t s = lo + add;
+    uint64_t c1 = s < lo;
+    uint64_t s2 = s + carry;
+    c1 += s2 < s;
+    out = s2;
+    carry = hi + c1;
+}
+
+__device__ __forceinline__ u64x2 ml_mont1(u64x2 a, u64x2 b, const MLConsts &c) {
+    uint64_t t0, t1, t2, t3, carry;
+    // mul_limbs
+    carry = 0;
+    mac(a.x, b.x, 0, carry, t0);
+    mac(a.x, b.y, 0, carry, t1);
+    t2 = carry;
+    carry = 0;
+    mac(a.y, b.x, t1, carry, t1);
+    mac(a.y, b.y, t2, carry, t2);
+    t3 = carry;
+    // reduce, i = 0
+    uint64_t m = t0 * c.qinv;
+    carry = 0;
+    mac(m, c.q0, t0, carry, t0);
+    mac(m, c.q1, t1, carry, t1);
+    if (carry) { uint64_t s = t2 + carry; carry = s < t2; t2 = s; }
+    if (carry) { uint64_t s = t3 + carry; carry = s < t3; t3 = s; }
+    // i = 1
+    m = t1 * c.qinv;
+    carry = 0;
+    mac(m, c.q0, t1, carry, t1);
+    mac(m, c.q1, t2, carry, t2);
+    if (carry) { uint64_t s = t3 + carry; t3 = s; }
+    u64x2 r;
+    r.x = t2;
+    r.y = t3;
+    const bool lt = (t3 < c.q1) || (t3 == c.q1 && t2 < c.q0);
+    if (!lt) {
+        const uint64_t d0 = t2 - c.q0;
+        const uint64_t borrow = t2 < c.q0;
+        r.x = d0;
+        r.y = t3 - c.q1 - borrow;
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_ml_montmul(const u64x2 *__restrict__ a, const u64x2 *__restrict__ b, u64x2 *__restrict__ c,
+             size_t n, MLConsts k) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const u64x2 x = __builtin_nontemporal_load(a + i);
+        const u64x2 y = __builtin_nontemporal_load(b + i);
+        __builtin_nontemporal_store(ml_mont1(x, y, k), c + i);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_decompose(const uint64_t *__restrict__ poly, uint64_t *__restrict__ out, uint32_t n, size_t npoly,
+            uint32_t base_log, uint32_t level, ModConsts m) {
+    const size_t total = (size_t)n * npoly;
+    const uint64_t base = 1ull << base_log, mask = base - 1, half = base / 2;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t p = i / n, x = i % n;
+        const uint64_t c = poly[i];
+        for (uint32_t l = 0; l < level; ++l) {
+            const uint32_t shift = (level - 1 - l) * base_log;
+            uint64_t d = (c >> shift) & mask;
+            if (d > half) {
+                d = m.q - (base - d);
+                if (d >= m.q) d = mod64_slow(d, m.q, m.mu);
+            }
+            out[(p * level + l) * n + x] = d;
+        }
+    }
+}
+
+hipError_t launch_modmul(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
+                         hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_modmul, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, b, c, n, m);
+    return hipGetLastError();
+}
+hipError_t launch_addsub(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n, int sub,
+                         hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_addsub, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, b, c, n, sub, m);
+    return hipGetLastError();
+}
+hipError_t launch_neg(uint64_t q, const uint64_t *a, uint64_t *c, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_neg, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, c, n, q);
+    return hipGetLastError();
+}
+hipError_t launch_mul_scalar(const ModConsts &m, const uint64_t *a, uint64_t sc, uint64_t sc_shoup, uint64_t *c,
+                             size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mul_scalar, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, c, n, sc, sc_shoup, m);
+    return hipGetLastError();
+}
+hipError_t launch_ml_montmul(const uint64_t consts[7], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    MLConsts k{consts[0], consts[1], consts[6]};
+    hipLaunchKernelGGL(k_ml_montmul, dim3(grid_for(n)), dim3(kBlock), 0, s, reinterpret_cast<const u64x2 *>(a),
+                       reinterpret_cast<const u64x2 *>(b), reinterpret_cast<u64x2 *>(c), n, k);
+    return hipGetLastError();
+}
+hipError_t launch_decompose(const ModConsts &m, const uint64_t *poly, uint64_t *out, uint32_t n, size_t npoly,
+                            uint32_t base_log, uint32_t level, hipStream_t s) {
+    if (n == 0 || npoly == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decompose, dim3(grid_for((size_t)n * npoly)), dim3(kBlock), 0, s, poly, out, n, npoly,
+                       base_log, level, m);
+    return hipGetLastError();
+}
+
+}  // namespace fhe

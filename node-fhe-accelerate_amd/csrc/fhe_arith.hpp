@@ -1,0 +1,91 @@
+// fhe_arith.hpp -- modular arithmetic for the gfx950 kernels.
+//
+// Two word sizes share one interface (struct Arith<W>):
+//   W = uint32_t : q < 2^30   (Harvey lazy butterflies need 4q < 2^32)
+//   W = uint64_t : q < 2^62   (4q < 2^64)
+// Coefficients stay in HBM as u64 in both cases (the reference's
+// Polynomial layout, polynomial_ring.h:31-93); the 32-bit path only narrows
+// registers and LDS.
+//
+// All reductions are exact over Z_q, so canonical outputs are bit-identical
+// to the reference's "%"-based arithmetic (ntt_processor.cpp:298-307,
+// polynomial_ring.cpp:512-526) even though the operation sequence differs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fhe {
+
+__device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
+__device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
+// unsigned min: x - k wraps above x when x < k, so min() keeps x.
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// Twiddle with its Shoup companion w' = floor(w * 2^W / q).
+template <typename W> struct Tw { W w, wp; };
+
+template <typename W>
+struct Arith {
+    W q, q2;      // q, 2q
+    W qinv;       // -q^-1 mod 2^W (Montgomery)
+    W r2;         // R^2 mod q, R = 2^W
+
+    // x in [0, 2^W): x*w mod q, lazy result in [0, 2q)   (Shoup)
+    __device__ __forceinline__ W shoup(W x, W w, W wp) const {
+        W h = mulhi(x, wp);
+        return x * w - h * q;
+    }
+    __device__ __forceinline__ W shoup(W x, Tw<W> t) const { return shoup(x, t.w, t.wp); }
+
+    // Montgomery: a*b*R^-1 mod q in [0, 2q); requires a*b < q*R.
+    __device__ __forceinline__ W mont(W a, W b) const {
+        W lo = a * b;
+        W hi = mulhi(a, b);
+        W m = lo * qinv;
+        return hi + mulhi(m, q) + (lo != 0 ? W(1) : W(0));
+    }
+
+    __device__ __forceinline__ W red2q(W x) const { return umin(x, W(x - q2)); }  // [0,4q)->[0,2q)
+    __device__ __forceinline__ W red1q(W x) const { return umin(x, W(x - q)); }   // [0,2q)->[0,q)
+    __device__ __forceinline__ W canon4(W x) const { return red1q(red2q(x)); }     // [0,4q)->[0,q)
+
+    // Harvey forward (Cooley-Tukey) butterfly, values in [0, 4q).
+    __device__ __forceinline__ void ct(W &x, W &y, Tw<W> t) const {
+        W a = red2q(x);
+        W b = shoup(y, t);
+        x = a + b;
+        y = a - b + q2;
+    }
+    // Gentleman-Sande butterfly, values in [0, 2q).
+    __device__ __forceinline__ void gs(W &x, W &y, Tw<W> t) const {
+        W s = x + y;
+        W d = x - y + q2;
+        x = red2q(s);
+        y = shoup(d, t);
+    }
+    // Last GS stage with the N^-1 scaling folded in (w = 1 at stage 0).
+    __device__ __forceinline__ void gs_scaled(W &x, W &y, Tw<W> ninv) const {
+        W s = x + y;
+        W d = x - y + q2;
+        x = shoup(s, ninv);
+        y = shoup(d, ninv);
+    }
+};
+
+// Exact 64-bit x mod q for any q >= 2 (slow path; taken only for inputs
+// outside the lazy range).  mu = floor(2^64 / q).
+__device__ __forceinline__ uint64_t mod64_slow(uint64_t x, uint64_t q, uint64_t mu) {
+    if (q >> 63) return x >= q ? x - q : x;
+    uint64_t r = x - __umul64hi(x, mu) * q;
+    return r >= q ? r - q : r;
+}
+
+// Load a u64 coefficient into the lazy range [0, lim) of word W.
+template <typename W>
+__device__ __forceinline__ W load_lazy(uint64_t x, uint64_t lim, uint64_t q, uint64_t mu) {
+    if (x >= lim) x = mod64_slow(x, q, mu);
+    return W(x);
+}
+
+}  // namespace fhe

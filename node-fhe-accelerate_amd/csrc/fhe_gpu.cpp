@@ -1,0 +1,732 @@
+// fhe_gpu.cpp -- host side of libfhe_gpu.so: the C ABI of include/fhe_gpu.h.
+//
+// Owns per-context twiddle tables in HBM, parameter validation with the
+// reference's messages, host<->device staging for FHE_HOST calls, and the
+// scalar N-API ModularArithmetic helpers.  All arithmetic on coefficient
+// vectors runs in the HIP kernels (ntt_*.hip, elementwise.hip); there is no
+// CPU fallback: without a usable device every compute entry point fails
+// with FHE_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fhe_gpu.h"
+#include "fhe_internal.hpp"
+
+using u64 = uint64_t;
+using u32 = uint32_t;
+using u128 = unsigned __int128;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char *what) {
+    return fail(FHE_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr, what)                      \
+    do {                                         \
+        hipError_t _e = (expr);                  \
+        if (_e != hipSuccess) return hip_fail(_e, what); \
+    } while (0)
+
+// ---------------------------------------------------------------- number theory (host)
+u64 mulmod(u64 a, u64 b, u64 q) { return (u64)((u128)a * b % q); }
+u64 powmod(u64 b, u64 e, u64 q) {
+    u64 r = 1 % q;
+    b %= q;
+    while (e) {
+        if (e & 1) r = mulmod(r, b, q);
+        b = mulmod(b, b, q);
+        e >>= 1;
+    }
+    return r;
+}
+// a^-1 mod q by extended Euclid on 128-bit signed values (exact for any q).
+bool invmod(u64 a, u64 q, u64 &out) {
+    __int128 t = 0, nt = 1, r = q, nr = a % q;
+    while (nr != 0) {
+        __int128 quo = r / nr, tmp;
+        tmp = t - quo * nt; t = nt; nt = tmp;
+        tmp = r - quo * nr; r = nr; nr = tmp;
+    }
+    if (r != 1) return false;
+    if (t < 0) t += q;
+    out = (u64)t;
+    return true;
+}
+template <typename W>
+W neg_inv_pow2(W q) {  // -q^-1 mod 2^W (q odd), Newton
+    W x = q;
+    for (int i = 0; i < 6; ++i) x *= W(2) - q * x;
+    return W(0) - x;
+}
+template <typename W>
+fhe::Tw<W> make_tw(u64 w, u64 q) {
+    constexpr int BITS = sizeof(W) * 8;
+    fhe::Tw<W> t;
+    t.w = (W)w;
+    t.wp = (W)(((u128)w << BITS) / q);
+    return t;
+}
+
+// ---------------------------------------------------------------- context
+struct Tables {
+    void *twf = nullptr, *twi = nullptr, *twist = nullptr, *untwist = nullptr, *untwist_r = nullptr;
+};
+
+}  // namespace
+
+struct fhe_ctx {
+    u32 n = 0, logn = 0;
+    u64 q = 0, psi = 0, psi_inv = 0, inv_n = 0;
+    int mode = 0, device = 0, word = 64;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    Tables tab;
+    fhe::Plan plan{};
+    std::vector<u64> fwd_tw, inv_tw;  // reference twiddle vectors (host copy)
+    std::mutex scratch_mu;
+    void *scratch[3] = {nullptr, nullptr, nullptr};
+    size_t scratch_bytes = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// NTTProcessor::find_primitive_root (ntt_processor.cpp:92-128): smallest
+// g >= 2 with psi = g^((q-1)/2N), psi^2N == 1, psi^N == q-1.  The search is
+// capped (the reference loops to q; a prime q finds g within a few tries).
+int find_psi(u32 n, u64 q, u64 &psi) {
+    const u64 two_n = (u64)n * 2;
+    if ((q - 1) % two_n != 0)
+        return fail(FHE_ERR_NOT_NTT_FRIENDLY, "Modulus is not NTT-friendly: q \xe2\x89\xa2 1 (mod 2N)");
+    const u64 e = (q - 1) / two_n;
+    const u64 cap = std::min<u64>(q, (u64)1 << 22);
+    for (u64 g = 2; g < cap; ++g) {
+        const u64 w = powmod(g, e, q);
+        if (powmod(w, two_n, q) == 1 && powmod(w, n, q) == q - 1) {
+            psi = w;
+            return FHE_OK;
+        }
+    }
+    return fail(FHE_ERR_NO_ROOT, "Could not find primitive root for given parameters");
+}
+
+template <typename W>
+int build_tables(fhe_ctx *c, fhe::NttArgs<W> &A) {
+    const u32 n = c->n, L = c->logn;
+    const u64 q = c->q;
+    constexpr int BITS = sizeof(W) * 8;
+    std::vector<fhe::Tw<W>> twf(n), twi(n), twist(n), untw(n), untw_r(n);
+    // stage-major: entry 2^s + j holds the twiddle of butterfly j in stage s
+    for (u32 s = 0; s < L; ++s) {
+        for (u32 j = 0; j < (1u << s); ++j) {
+            // compat: psi^(j*N/2^(s+1)); negacyclic: (psi^2)^(j*N/2^(s+1))
+            const u64 ex = c->mode == FHE_MODE_COMPAT ? (u64)j * (n >> (s + 1)) : (u64)j * (n >> s);
+            twf[(1u << s) + j] = make_tw<W>(c->fwd_tw[ex], q);
+            twi[(1u << s) + j] = make_tw<W>(c->inv_tw[ex], q);
+        }
+    }
+    twf[0] = make_tw<W>(1, q);
+    twi[0] = make_tw<W>(1, q);
+    const u64 R = (u64)((((u128)1) << BITS) % q);
+    const u64 ninv_r = mulmod(c->inv_n, R, q);
+    for (u32 i = 0; i < n; ++i) {
+        twist[i] = make_tw<W>(c->fwd_tw[i], q);
+        const u64 u = mulmod(c->inv_tw[i], c->inv_n, q);
+        untw[i] = make_tw<W>(u, q);
+        untw_r[i] = make_tw<W>(mulmod(u, R, q), q);
+    }
+    const size_t bytes = sizeof(fhe::Tw<W>) * n;
+    void **dst[5] = {&c->tab.twf, &c->tab.twi, &c->tab.twist, &c->tab.untwist, &c->tab.untwist_r};
+    const void *srcs[5] = {twf.data(), twi.data(), twist.data(), untw.data(), untw_r.data()};
+    for (int i = 0; i < 5; ++i) {
+        HIP_TRY(hipMalloc(dst[i], bytes), "hipMalloc(twiddles)");
+        HIP_TRY(hipMemcpy(*dst[i], srcs[i], bytes, hipMemcpyHostToDevice), "hipMemcpy(twiddles)");
+    }
+    A.twf = (const fhe::Tw<W> *)c->tab.twf;
+    A.twi = (const fhe::Tw<W> *)c->tab.twi;
+    A.twist = (const fhe::Tw<W> *)c->tab.twist;
+    A.untwist = (const fhe::Tw<W> *)c->tab.untwist;
+    A.untwist_r = (const fhe::Tw<W> *)c->tab.untwist_r;
+    A.ar.q = (W)q;
+    A.ar.q2 = (W)(2 * q);
+    A.ar.qinv = neg_inv_pow2<W>((W)q);
+    A.ar.r2 = (W)mulmod(R, R, q);
+    A.q64 = q;
+    A.mu64 = (u64)((((u128)1) << 64) / q);
+    A.ninv = make_tw<W>(c->inv_n, q);
+    A.ninv_r = make_tw<W>(ninv_r, q);
+    A.rmod = make_tw<W>(R, q);
+    return FHE_OK;
+}
+
+void free_tables(fhe_ctx *c) {
+    void *p[5] = {c->tab.twf, c->tab.twi, c->tab.twist, c->tab.untwist, c->tab.untwist_r};
+    for (void *x : p)
+        if (x) (void)hipFree(x);
+    c->tab = Tables{};
+    for (auto &s : c->scratch)
+        if (s) { (void)hipFree(s); s = nullptr; }
+}
+
+fhe::ModConsts mod_consts(u64 q) {
+    fhe::ModConsts m{};
+    m.q = q;
+    m.mu = q > 1 ? (u64)((((u128)1) << 64) / q) : 0;
+    m.fast = (q & 1) && q > 1 && !(q >> 63);
+    if (m.fast) {
+        m.qinv = neg_inv_pow2<u64>(q);
+        const u64 R = (u64)((((u128)1) << 64) % q);
+        m.r2 = mulmod(R, R, q);
+    }
+    return m;
+}
+
+int check_ctx(const fhe_ctx *c) {
+    if (!c) return fail(FHE_ERR_INVALID_ARG, "null context");
+    return FHE_OK;
+}
+
+// Host staging: run fn(device pointers) over chunks of at most `chunk` polys.
+// nin inputs, one output; all of n*batch u64 per buffer (or `elems` each).
+template <typename F>
+int staged(fhe_ctx *c, const u64 *const *ins, int nin, size_t in_elems_per_unit, u64 *out,
+           size_t out_elems_per_unit, size_t units, F &&fn) {
+    std::lock_guard<std::mutex> lk(c->scratch_mu);
+    const size_t max_unit_bytes = std::max(in_elems_per_unit, out_elems_per_unit) * sizeof(u64);
+    size_t chunk = std::max<size_t>(1, ((size_t)256 << 20) / max_unit_bytes);
+    chunk = std::min(chunk, units);
+    const size_t need = chunk * max_unit_bytes;
+    if (c->scratch_bytes < need) {
+        for (auto &s : c->scratch)
+            if (s) { (void)hipFree(s); s = nullptr; }
+        c->scratch_bytes = 0;
+        for (auto &s : c->scratch) HIP_TRY(hipMalloc(&s, need), "hipMalloc(scratch)");
+        c->scratch_bytes = need;
+    }
+    for (size_t u0 = 0; u0 < units; u0 += chunk) {
+        const size_t nu = std::min(chunk, units - u0);
+        const u64 *dins[3] = {nullptr, nullptr, nullptr};
+        for (int i = 0; i < nin; ++i) {
+            HIP_TRY(hipMemcpyAsync(c->scratch[i], ins[i] + u0 * in_elems_per_unit, nu * in_elems_per_unit * 8,
+                                   hipMemcpyHostToDevice, c->stream),
+                    "hipMemcpyAsync(H2D)");
+            dins[i] = (const u64 *)c->scratch[i];
+        }
+        u64 *dout = (u64 *)c->scratch[2];
+        HIP_TRY(fn(dins, dout, nu), "kernel launch");
+        HIP_TRY(hipMemcpyAsync(out + u0 * out_elems_per_unit, dout, nu * out_elems_per_unit * 8,
+                               hipMemcpyDeviceToHost, c->stream),
+                "hipMemcpyAsync(D2H)");
+        HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
+    return FHE_OK;
+}
+
+// Common driver for ops over [batch][n] buffers.
+template <typename F>
+int run_poly_op(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, size_t batch, int where, size_t in_per,
+                size_t out_per, F &&fn) {
+    if (int rc = check_ctx(c)) return rc;
+    if ((!a && batch) || (!out && batch)) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    if (where != FHE_HOST && where != FHE_DEVICE) return fail(FHE_ERR_INVALID_ARG, "where must be FHE_HOST or FHE_DEVICE");
+    if (batch == 0) return FHE_OK;
+    DeviceGuard g(c->device);
+    if (where == FHE_DEVICE) {
+        const u64 *ins[3] = {a, b, nullptr};
+        HIP_TRY(fn(ins, out, batch), "kernel launch");
+        return FHE_OK;
+    }
+    const u64 *ins[2] = {a, b};
+    return staged(c, ins, b ? 2 : 1, in_per, out, out_per, batch, fn);
+}
+
+}  // namespace
+
+// =====================================================================
+extern "C" {
+
+const char *fhe_last_error(void) { return g_err.c_str(); }
+const char *fhe_version(void) { return "fhe-mi355x 0.1.0 (gfx950)"; }
+
+int fhe_detect(fhe_hw_caps *caps) {
+    if (!caps) return fail(FHE_ERR_INVALID_ARG, "null caps");
+    std::memset(caps, 0, sizeof(*caps));
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    caps->device_count = count;
+    if (count > 0) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, 0) == hipSuccess) {
+            caps->compute_units = p.multiProcessorCount;
+            caps->wavefront_size = p.warpSize;
+            caps->hbm_bytes = p.totalGlobalMem;
+            caps->lds_bytes_per_cu = p.maxSharedMemoryPerMultiProcessor;
+            std::snprintf(caps->arch, sizeof(caps->arch), "%s", p.gcnArchName);
+            std::snprintf(caps->name, sizeof(caps->name), "%s", p.name);
+            caps->xcds = std::strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 8 : 1;
+        }
+    }
+    return FHE_OK;
+}
+
+int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) {
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    // NTTProcessor constructor validation order (ntt_processor.cpp:140-153)
+    if (n == 0 || (n & (n - 1)) != 0) return fail(FHE_ERR_DEGREE_POW2, "Polynomial degree must be a power of 2");
+    if (n < 4 || n > 65536) return fail(FHE_ERR_DEGREE_RANGE, "Polynomial degree must be between 4 and 65536");
+    if ((q & 1) == 0) return fail(FHE_ERR_MODULUS_EVEN, "Modulus must be odd");
+    if (mode != FHE_MODE_COMPAT && mode != FHE_MODE_NEGACYCLIC) return fail(FHE_ERR_INVALID_ARG, "unknown mode");
+    u64 psi = 0;
+    if (int rc = find_psi(n, q, psi)) return rc;
+    u32 logn = 0;
+    while ((1u << logn) < n) ++logn;
+    if ((int)logn > fhe::kMaxLogN)
+        return fail(FHE_ERR_UNSUPPORTED, "GPU kernels implement degrees up to 16384 (got " + std::to_string(n) + ")");
+    if (q >> 62) return fail(FHE_ERR_UNSUPPORTED, "GPU kernels implement moduli below 2^62");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(FHE_ERR_DEVICE, "no HIP device available (the backend has no CPU fallback)");
+    if (device < 0 || device >= count) return fail(FHE_ERR_INVALID_ARG, "device ordinal out of range");
+
+    fhe_ctx *c = new fhe_ctx();
+    c->n = n; c->logn = logn; c->q = q; c->psi = psi; c->mode = mode; c->device = device;
+    c->word = q < (1ull << 30) ? 32 : 64;
+    if (!invmod(psi, q, c->psi_inv) || !invmod(n, q, c->inv_n)) {
+        delete c;
+        return fail(FHE_ERR_NO_ROOT, "Could not find primitive root for given parameters");
+    }
+    c->fwd_tw.resize(n);
+    c->inv_tw.resize(n);
+    c->fwd_tw[0] = c->inv_tw[0] = 1;
+    for (u32 i = 1; i < n; ++i) {
+        c->fwd_tw[i] = mulmod(c->fwd_tw[i - 1], psi, q);
+        c->inv_tw[i] = mulmod(c->inv_tw[i - 1], c->psi_inv, q);
+    }
+    DeviceGuard g(device);
+    int rc = c->word == 32 ? build_tables<u32>(c, c->plan.a32) : build_tables<u64>(c, c->plan.a64);
+    if (rc == FHE_OK) {
+        hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+        if (e != hipSuccess) rc = hip_fail(e, "hipStreamCreate");
+    }
+    if (rc != FHE_OK) {
+        free_tables(c);
+        delete c;
+        return rc;
+    }
+    c->stream = c->own_stream;
+    c->plan.logn = logn;
+    c->plan.word = c->word;
+    c->plan.nega = mode;
+    c->plan.stream = c->stream;
+    *out = c;
+    return FHE_OK;
+}
+
+void fhe_ctx_destroy(fhe_ctx *c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_tables(c);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int fhe_ctx_set_stream(fhe_ctx *c, void *s) {
+    if (int rc = check_ctx(c)) return rc;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->plan.stream = c->stream;
+    return FHE_OK;
+}
+void *fhe_ctx_stream(const fhe_ctx *c) { return c ? (void *)c->stream : nullptr; }
+int fhe_ctx_synchronize(fhe_ctx *c) {
+    if (int rc = check_ctx(c)) return rc;
+    DeviceGuard g(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    return FHE_OK;
+}
+
+int fhe_ctx_get_info(const fhe_ctx *c, fhe_ctx_info *info) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!info) return fail(FHE_ERR_INVALID_ARG, "null info");
+    info->n = c->n; info->log_n = c->logn; info->q = c->q; info->psi = c->psi; info->psi_inv = c->psi_inv;
+    info->inv_n = c->inv_n; info->mode = c->mode; info->word_bits = c->word; info->device = c->device;
+    const int loge = c->logn < 4 ? (int)c->logn : 4;
+    const int t = 1 << (c->logn - loge);
+    info->polys_per_block = t >= 256 ? 1 : 256 / t;
+    info->threads_per_block = t * info->polys_per_block;
+    return FHE_OK;
+}
+
+int fhe_ctx_get_twiddles(const fhe_ctx *c, uint64_t *fwd, uint64_t *inv) {
+    if (int rc = check_ctx(c)) return rc;
+    if (fwd) std::memcpy(fwd, c->fwd_tw.data(), 8 * c->n);
+    if (inv) std::memcpy(inv, c->inv_tw.data(), 8 * c->n);
+    return FHE_OK;
+}
+
+int fhe_ntt_fwd_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return fhe::launch_fwd(c->plan, d[0], o, nb, 0); });
+}
+int fhe_ntt_inv_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return fhe::launch_inv(c->plan, d[0], o, nb); });
+}
+int fhe_ntt_fwd_mul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!w && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    return run_poly_op(c, a, w, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_fwd_mul(c->plan, d[0], d[1], o, nb);
+    });
+}
+int fhe_polymul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_polymul(c->plan, d[0], d[1], o, nb);
+    });
+}
+int fhe_pointwise_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const fhe::ModConsts m = mod_consts(c->q);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_modmul(m, d[0], d[1], o, nb * c->n, c->stream);
+    });
+}
+int fhe_poly_add_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const fhe::ModConsts m = mod_consts(c->q);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_addsub(m, d[0], d[1], o, nb * c->n, 0, c->stream);
+    });
+}
+int fhe_poly_sub_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const fhe::ModConsts m = mod_consts(c->q);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_addsub(m, d[0], d[1], o, nb * c->n, 1, c->stream);
+    });
+}
+int fhe_poly_neg_batch(fhe_ctx *c, const uint64_t *a, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_neg(c->q, d[0], o, nb * c->n, c->stream);
+    });
+}
+int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, uint64_t *out, size_t batch,
+                              int where) {
+    if (int rc = check_ctx(c)) return rc;
+    const fhe::ModConsts m = mod_consts(c->q);
+    const u64 s = scalar % c->q;
+    const u64 sp = (u64)(((u128)s << 64) / c->q);
+    return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_mul_scalar(m, d[0], s, sp, o, nb * c->n, c->stream);
+    });
+}
+
+static int check_decomp(uint32_t k, uint32_t base_log, uint32_t level) {
+    if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
+    if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
+        return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    return FHE_OK;
+}
+
+int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggsw, uint64_t *ggsw_ntt, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
+    if (level == 0) return fail(FHE_ERR_INVALID_ARG, "level must be >= 1");
+    const size_t polys = (size_t)(k + 1) * level * (k + 1);
+    return run_poly_op(c, ggsw, nullptr, ggsw_ntt, polys, where, c->n, c->n,
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return fhe::launch_fwd(c->plan, d[0], o, nb, 1); });
+}
+
+int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
+                               const uint64_t *ggsw_ntt, uint64_t *out, size_t batch, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (int rc = check_decomp(k, base_log, level)) return rc;
+    if (!ggsw_ntt && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const size_t per = (size_t)(k + 1) * c->n;
+    if (where == FHE_HOST && batch) {
+        // the key is shared by every ciphertext: upload it once
+        DeviceGuard g(c->device);
+        const size_t kbytes = (size_t)(k + 1) * level * (k + 1) * c->n * 8;
+        void *dk = nullptr;
+        HIP_TRY(hipMalloc(&dk, kbytes), "hipMalloc(ggsw)");
+        hipError_t e = hipMemcpy(dk, ggsw_ntt, kbytes, hipMemcpyHostToDevice);
+        int rc = e != hipSuccess ? hip_fail(e, "hipMemcpy(ggsw)") : FHE_OK;
+        if (rc == FHE_OK)
+            rc = run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb) {
+                return fhe::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], (const u64 *)dk, o, nb);
+            });
+        (void)hipFree(dk);
+        return rc;
+    }
+    return run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb) {
+        return fhe::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], ggsw_ntt, o, nb);
+    });
+}
+
+int fhe_decompose_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *poly, uint64_t *out,
+                        size_t npoly, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
+        return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    const fhe::ModConsts m = mod_consts(c->q);
+    return run_poly_op(c, poly, nullptr, out, npoly, where, c->n, (size_t)c->n * level,
+                       [&](const u64 *const *d, u64 *o, size_t nb) {
+                           return fhe::launch_decompose(m, d[0], o, c->n, nb, base_log, level, c->stream);
+                       });
+}
+
+// ---------------------------------------------------------------- context-free kernels
+static int run_flat(int device, void *stream, int where, const u64 *a, const u64 *b, u64 *c, size_t count,
+                    size_t width, hipError_t (*fn)(const void *, const u64 *, const u64 *, u64 *, size_t, hipStream_t),
+                    const void *arg) {
+    if (where != FHE_HOST && where != FHE_DEVICE) return fail(FHE_ERR_INVALID_ARG, "where must be FHE_HOST or FHE_DEVICE");
+    if (count == 0) return FHE_OK;
+    if (!a || !b || !c) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(FHE_ERR_DEVICE, "no HIP device available (the backend has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(FHE_ERR_INVALID_ARG, "device ordinal out of range");
+    DeviceGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    if (where == FHE_DEVICE) {
+        HIP_TRY(fn(arg, a, b, c, count, s), "kernel launch");
+        return FHE_OK;
+    }
+    const size_t bytes = count * width * 8;
+    void *da = nullptr, *db = nullptr, *dc = nullptr;
+    hipError_t e = hipMalloc(&da, bytes);
+    if (e == hipSuccess) e = hipMalloc(&db, bytes);
+    if (e == hipSuccess) e = hipMalloc(&dc, bytes);
+    if (e == hipSuccess) e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = fn(arg, (const u64 *)da, (const u64 *)db, (u64 *)dc, count, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipMemcpy(c, dc, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc);
+    if (e != hipSuccess) return hip_fail(e, "modular kernel");
+    return FHE_OK;
+}
+
+static hipError_t modmul_thunk(const void *arg, const u64 *a, const u64 *b, u64 *c, size_t n, hipStream_t s) {
+    return fhe::launch_modmul(*(const fhe::ModConsts *)arg, a, b, c, n, s);
+}
+int fhe_modmul_batch(uint64_t q, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t count, int where,
+                     int device, void *stream) {
+    if (q == 0) return fail(FHE_ERR_ZERO_MODULUS, "Modulus must be non-zero for Barrett reduction");
+    const fhe::ModConsts m = mod_consts(q);
+    return run_flat(device, stream, where, a, b, c, count, 1, modmul_thunk, &m);
+}
+
+// MultiLimbMontgomeryConstants (modular_arithmetic.cpp:471-486) with 2 limbs,
+// including multi_limb_mod_proper's truncated shifted modulus and strict
+// comparison (:361-429), so the constants match the reference bit for bit.
+static void ml_reduce(const u64 *a, size_t asz, const u64 *mod, u64 *out) {
+    const size_t nl = 2, rs = std::max(asz, nl);
+    u64 rem[4] = {0, 0, 0, 0};
+    std::memcpy(rem, a, asz * 8);
+    if (asz <= nl) {
+        const u64 hi = asz > 1 ? a[1] : 0;
+        if (hi < mod[1] || (hi == mod[1] && a[0] < mod[0])) {
+            out[0] = a[0];
+            out[1] = hi;
+            return;
+        }
+    }
+    for (int bp = (int)(rs * 64) - 1; bp >= 0; --bp) {
+        const size_t ls = (size_t)bp / 64, bs = (size_t)bp % 64;
+        u64 sh[4] = {0, 0, 0, 0};
+        for (size_t i = 0; i < nl && i + ls < rs; ++i) {
+            if (bs == 0) sh[i + ls] = mod[i];
+            else {
+                sh[i + ls] |= mod[i] << bs;
+                if (i + ls + 1 < rs) sh[i + ls + 1] = mod[i] >> (64 - bs);
+            }
+        }
+        bool can = false;
+        for (int i = (int)rs - 1; i >= 0; --i) {
+            if (rem[i] > sh[i]) { can = true; break; }
+            if (rem[i] < sh[i]) break;
+        }
+        if (can) {
+            u64 borrow = 0;
+            for (size_t i = 0; i < rs; ++i) {
+                const u64 r = rem[i], s = sh[i];
+                rem[i] = r - s - borrow;
+                borrow = (r < s + borrow) ? 1 : 0;
+            }
+        }
+    }
+    out[0] = rem[0];
+    out[1] = rem[1];
+}
+
+int fhe_ml_constants(const uint64_t q[2], uint64_t out[7]) {
+    if (!q || !out) return fail(FHE_ERR_INVALID_ARG, "null argument");
+    if ((q[0] == 0 && q[1] == 0) || (q[0] & 1) == 0)
+        return fail(FHE_ERR_MONT_MODULUS, "Modulus must be odd and non-zero for Montgomery arithmetic");
+    const u64 rl[3] = {0, 0, 1};
+    u64 r[2], r2[2];
+    ml_reduce(rl, 3, q, r);
+    u64 prod[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 2; ++i) {
+        u64 carry = 0;
+        for (int j = 0; j < 2; ++j) {
+            u128 p = (u128)r[i] * r[j] + prod[i + j] + carry;
+            prod[i + j] = (u64)p;
+            carry = (u64)(p >> 64);
+        }
+        prod[i + 2] = carry;
+    }
+    ml_reduce(prod, 4, q, r2);
+    u64 x = q[0];
+    for (int i = 0; i < 5; ++i) x = x * (2 - q[0] * x);
+    out[0] = q[0]; out[1] = q[1]; out[2] = r[0]; out[3] = r[1]; out[4] = r2[0]; out[5] = r2[1];
+    out[6] = (~x) + 1;
+    return FHE_OK;
+}
+
+static hipError_t ml_thunk(const void *arg, const u64 *a, const u64 *b, u64 *c, size_t n, hipStream_t s) {
+    return fhe::launch_ml_montmul((const u64 *)arg, a, b, c, n, s);
+}
+int fhe_ml_montmul_batch(const uint64_t q[2], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t count,
+                         int where, int device, void *stream) {
+    u64 consts[7];
+    if (int rc = fhe_ml_constants(q, consts)) return rc;
+    return run_flat(device, stream, where, a, b, c, count, 2, ml_thunk, consts);
+}
+
+// ---------------------------------------------------------------- N-API ModularArithmetic (scalar)
+// modular_arithmetic.cpp:8-31 extended Euclid with unsigned a, m and signed
+// x0/x1 (m0 = (int64)m).  A zero divisor (gcd(q, 2^64-1) > 1) traps on x86
+// in the reference; here it takes the AArch64 result (x/0 = 0, x%0 = x), the
+// platform the reference ships for.
+static u64 compat_mod_inverse(u64 a, u64 m) {
+    if (m == 0) return 0;
+    const int64_t m0 = (int64_t)m;
+    int64_t x0 = 0, x1 = 1;
+    if (m == 1) return 0;
+    while (a > 1) {
+        const int64_t qq = (int64_t)(m == 0 ? 0 : a / m);
+        int64_t t = (int64_t)m;
+        m = m == 0 ? a : a % m;
+        a = (u64)t;
+        t = x0;
+        x0 = (int64_t)((u64)x1 - (u64)qq * (u64)x0);
+        x1 = t;
+    }
+    if (x1 < 0) x1 = (int64_t)((u64)x1 + (u64)m0);
+    return (u64)x1;
+}
+
+int fhe_mont_constants_compat(uint64_t q, uint64_t k[4]) {
+    if (!k) return fail(FHE_ERR_INVALID_ARG, "null argument");
+    if (q == 0 || (q & 1) == 0)
+        return fail(FHE_ERR_MONT_MODULUS, "Modulus must be odd and non-zero for Montgomery arithmetic");
+    const u64 rq = (u64)((((u128)1) << 64) % q);
+    k[0] = q;
+    k[1] = rq;
+    k[2] = (u64)((u128)rq * rq % q);
+    k[3] = (~compat_mod_inverse(q, UINT64_MAX)) + 1;
+    return FHE_OK;
+}
+static u64 compat_reduce(const u64 k[4], u64 hi, u64 lo) {  // :84-111
+    const u64 m = lo * k[3];
+    const u128 mq = (u128)m * k[0];
+    const u128 sum = ((u128)hi << 64) + lo + mq;
+    u64 t = (u64)(sum >> 64);
+    if (t >= k[0]) t -= k[0];
+    return t;
+}
+uint64_t fhe_compat_montgomery_mul(const uint64_t k[4], uint64_t a, uint64_t b) {
+    const u128 p = (u128)a * b;
+    return compat_reduce(k, (u64)(p >> 64), (u64)p);
+}
+uint64_t fhe_compat_to_montgomery(const uint64_t k[4], uint64_t a) { return fhe_compat_montgomery_mul(k, a, k[2]); }
+uint64_t fhe_compat_from_montgomery(const uint64_t k[4], uint64_t a) { return compat_reduce(k, 0, a); }
+uint64_t fhe_compat_mod_add(uint64_t q, uint64_t a, uint64_t b) {
+    a %= q; b %= q;
+    u64 s = a + b;
+    if (s < a || s >= q) s -= q;
+    return s;
+}
+uint64_t fhe_compat_mod_sub(uint64_t q, uint64_t a, uint64_t b) {
+    a %= q; b %= q;
+    return a >= b ? a - b : q - (b - a);
+}
+
+// ---------------------------------------------------------------- memory / events
+int fhe_dev_alloc(int device, size_t bytes, void **out) {
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null out");
+    DeviceGuard g(device);
+    hipError_t e = hipMalloc(out, bytes);
+    if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMalloc: out of memory");
+    HIP_TRY(e, "hipMalloc");
+    return FHE_OK;
+}
+int fhe_dev_free(void *p) {
+    if (p) HIP_TRY(hipFree(p), "hipFree");
+    return FHE_OK;
+}
+int fhe_memcpy_h2d(void *d, const void *s, size_t b) {
+    HIP_TRY(hipMemcpy(d, s, b, hipMemcpyHostToDevice), "hipMemcpy(H2D)");
+    return FHE_OK;
+}
+int fhe_memcpy_d2h(void *d, const void *s, size_t b) {
+    HIP_TRY(hipMemcpy(d, s, b, hipMemcpyDeviceToHost), "hipMemcpy(D2H)");
+    return FHE_OK;
+}
+int fhe_device_synchronize(int device) {
+    DeviceGuard g(device);
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    return FHE_OK;
+}
+int fhe_event_create(void **ev) {
+    if (!ev) return fail(FHE_ERR_INVALID_ARG, "null out");
+    HIP_TRY(hipEventCreate((hipEvent_t *)ev), "hipEventCreate");
+    return FHE_OK;
+}
+int fhe_event_destroy(void *ev) {
+    if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy");
+    return FHE_OK;
+}
+int fhe_event_record(void *ev, void *s) {
+    HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)s), "hipEventRecord");
+    return FHE_OK;
+}
+int fhe_event_elapsed_ms(void *a, void *b, float *ms) {
+    HIP_TRY(hipEventSynchronize((hipEvent_t)b), "hipEventSynchronize");
+    HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
+    return FHE_OK;
+}
+
+}  // extern "C"

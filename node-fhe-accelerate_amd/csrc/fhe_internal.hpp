@@ -1,0 +1,53 @@
+// fhe_internal.hpp -- interface between the host C-ABI (fhe_gpu.cpp) and the
+// kernel translation units.  Not installed; no torch types anywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ntt_core.hpp"
+
+namespace fhe {
+
+struct Plan {
+    uint32_t logn;
+    int word;   // 32 or 64
+    int nega;   // 0 = compat, 1 = negacyclic
+    hipStream_t stream;
+    NttArgs<uint32_t> a32;
+    NttArgs<uint64_t> a64;
+};
+
+constexpr int kMinLogN = 2;
+constexpr int kMaxLogN = 14;
+
+// Forward NTT; epi 0: canonical output, 1: output * R mod q (Montgomery
+// form, used to prepare GGSW keys).
+hipError_t launch_fwd(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch, int epi);
+hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch);
+// out = fwd(a) (.) w  (config C3: NTT + modmul)
+hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch);
+// c = inv(fwd(a) (.) fwd(b))  (PolynomialRing::multiply)
+hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
+// TFHE external product, GGSW already in NTT-Montgomery form.
+hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const uint64_t *glwe,
+                          const uint64_t *ggsw, uint64_t *out, size_t batch);
+
+// Elementwise kernels (elementwise.hip).
+struct ModConsts {
+    uint64_t q, mu, qinv, r2;  // mu = floor(2^64/q); Montgomery R = 2^64
+    int fast;                  // q odd and q < 2^63
+};
+hipError_t launch_modmul(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
+                         hipStream_t s);
+hipError_t launch_addsub(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n, int sub,
+                         hipStream_t s);
+hipError_t launch_neg(uint64_t q, const uint64_t *a, uint64_t *c, size_t n, hipStream_t s);
+hipError_t launch_mul_scalar(const ModConsts &m, const uint64_t *a, uint64_t sc, uint64_t sc_shoup, uint64_t *c,
+                             size_t n, hipStream_t s);
+hipError_t launch_ml_montmul(const uint64_t consts[7], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
+                             hipStream_t s);
+hipError_t launch_decompose(const ModConsts &m, const uint64_t *poly, uint64_t *out, uint32_t n, size_t npoly,
+                            uint32_t base_log, uint32_t level, hipStream_t s);
+
+}  // namespace fhe

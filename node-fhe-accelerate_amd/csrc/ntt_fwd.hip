@@ -1,0 +1,101 @@
+// ntt_fwd.hip -- forward NTT kernels: plain (NTTProcessor::forward_ntt,
+// ntt_processor.cpp:262-311), Montgomery-prepared, and forward + pointwise
+// modmul (config C3: to_ntt then PolynomialRing::pointwise_multiply,
+// polynomial_ring.cpp:104-116, 493-530).
+#include "fhe_internal.hpp"
+
+namespace fhe {
+
+template <int LOGN, typename W, bool NEGA, int EPI>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    __shared__ W lds_all[G::P * G::N];
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t poly = (size_t)blockIdx.x * G::P + pl;
+    const bool valid = poly < batch;
+    W *lds = lds_all + pl * G::N;
+    W v[G::E];
+    fwd_poly<LOGN, NEGA>(lds, v, tau, in + poly * G::N, valid, A);
+    if (!valid) return;
+    uint64_t *dst = out + poly * G::N;
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        W x = v[e];
+        if constexpr (EPI == 1) x = A.ar.red1q(A.ar.shoup(x, A.rmod));
+        else x = A.ar.canon4(x);
+        __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, e));
+    }
+}
+
+template <int LOGN, typename W, bool NEGA>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
+              size_t batch, NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    __shared__ W lds_all[G::P * G::N];
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t poly = (size_t)blockIdx.x * G::P + pl;
+    const bool valid = poly < batch;
+    W *lds = lds_all + pl * G::N;
+    W v[G::E];
+    fwd_poly<LOGN, NEGA>(lds, v, tau, in + poly * G::N, valid, A);
+    if (!valid) return;
+    const uint64_t *wp = wv + poly * G::N;
+    uint64_t *dst = out + poly * G::N;
+    const uint64_t wlim = (uint64_t)(W)~W(0);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
+        // w * R mod q (Montgomery form) in [0, 2q); exact for any u64 w.
+        W wm = A.ar.mont(load_lazy<W>(__builtin_nontemporal_load(wp + gi), wlim, A.q64, A.mu64), A.ar.r2);
+        W x = A.ar.red1q(A.ar.mont(A.ar.red2q(v[e]), wm));
+        __builtin_nontemporal_store((uint64_t)x, dst + gi);
+    }
+}
+
+template <int LOGN, typename W, bool NEGA>
+static hipError_t fwd_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *in, uint64_t *out, size_t batch,
+                          int epi, const uint64_t *wv) {
+    using G = Geo<LOGN>;
+    const size_t blocks = (batch + G::P - 1) / G::P;
+    if (wv)
+        hipLaunchKernelGGL((k_ntt_fwd_mul<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, in, wv, out, batch, A);
+    else if (epi == 1)
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, 1>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
+    else
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, 0>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
+    return hipGetLastError();
+}
+
+template <typename W, bool NEGA>
+static hipError_t fwd_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_t *in, uint64_t *out, size_t batch,
+                               int epi, const uint64_t *wv) {
+    switch (p.logn) {
+#define FHE_CASE(L) \
+    case L: return fwd_one<L, W, NEGA>(A, p.stream, in, out, batch, epi, wv);
+        FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
+        FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
+#undef FHE_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+static hipError_t fwd_any(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch, int epi,
+                          const uint64_t *wv) {
+    if (batch == 0) return hipSuccess;
+    if (p.word == 32)
+        return p.nega ? fwd_dispatch<uint32_t, true>(p, p.a32, in, out, batch, epi, wv)
+                      : fwd_dispatch<uint32_t, false>(p, p.a32, in, out, batch, epi, wv);
+    return p.nega ? fwd_dispatch<uint64_t, true>(p, p.a64, in, out, batch, epi, wv)
+                  : fwd_dispatch<uint64_t, false>(p, p.a64, in, out, batch, epi, wv);
+}
+
+hipError_t launch_fwd(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch, int epi) {
+    return fwd_any(p, in, out, batch, epi, nullptr);
+}
+hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch) {
+    return fwd_any(p, a, out, batch, 0, w);
+}
+
+}  // namespace fhe

@@ -1,0 +1,92 @@
+// ntt_inv.hip -- inverse NTT (NTTProcessor::inverse_ntt,
+// ntt_processor.cpp:325-380) and the fused polynomial multiply
+// (PolynomialRing::multiply, polynomial_ring.cpp:421-447:
+// inv(fwd(a) (.) fwd(b)) in ONE kernel: both spectra stay in VGPRs, the
+// pointwise product is a Montgomery multiply whose R^-1 is folded into the
+// inverse's N^-1 scaling).
+#include "fhe_internal.hpp"
+
+namespace fhe {
+
+template <int LOGN, typename W, bool NEGA>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    __shared__ W lds_all[G::P * G::N];
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t poly = (size_t)blockIdx.x * G::P + pl;
+    const bool valid = poly < batch;
+    W *lds = lds_all + pl * G::N;
+    W v[G::E];
+    const uint64_t *src = in + poly * G::N;
+    const uint64_t lim = (uint64_t)A.ar.q2;  // GS inputs must be < 2q
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        uint64_t x = valid ? __builtin_nontemporal_load(src + gidx<LOGN, G::NP - 1>(tau, e)) : 0;
+        v[e] = load_lazy<W>(x, lim, A.q64, A.mu64);
+    }
+    inv_poly_from_regs<LOGN, NEGA>(lds, v, tau, out + poly * G::N, valid, A, A.ninv, A.untwist);
+}
+
+template <int LOGN, typename W, bool NEGA>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *__restrict__ c, size_t batch,
+          NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    __shared__ W lds_all[G::P * G::N];
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t poly = (size_t)blockIdx.x * G::P + pl;
+    const bool valid = poly < batch;
+    W *lds = lds_all + pl * G::N;
+    W va[G::E], vb[G::E];
+    fwd_poly<LOGN, NEGA>(lds, va, tau, a + poly * G::N, valid, A);
+    if constexpr (G::NP > 1) __syncthreads();  // LDS is reused by the second transform
+    fwd_poly<LOGN, NEGA>(lds, vb, tau, b + poly * G::N, valid, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) vb[e] = A.ar.mont(A.ar.red2q(va[e]), A.ar.red2q(vb[e]));  // a*b*R^-1
+    if constexpr (G::NP > 1) __syncthreads();
+    inv_poly_from_regs<LOGN, NEGA>(lds, vb, tau, c + poly * G::N, valid, A, A.ninv_r, A.untwist_r);
+}
+
+template <int LOGN, typename W, bool NEGA>
+static hipError_t inv_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *a, const uint64_t *b, uint64_t *c,
+                          size_t batch) {
+    using G = Geo<LOGN>;
+    const size_t blocks = (batch + G::P - 1) / G::P;
+    if (b)
+        hipLaunchKernelGGL((k_polymul<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, b, c, batch, A);
+    else
+        hipLaunchKernelGGL((k_ntt_inv<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, c, batch, A);
+    return hipGetLastError();
+}
+
+template <typename W, bool NEGA>
+static hipError_t inv_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_t *a, const uint64_t *b,
+                               uint64_t *c, size_t batch) {
+    switch (p.logn) {
+#define FHE_CASE(L) \
+    case L: return inv_one<L, W, NEGA>(A, p.stream, a, b, c, batch);
+        FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
+        FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
+#undef FHE_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+static hipError_t inv_any(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch) {
+    if (batch == 0) return hipSuccess;
+    if (p.word == 32)
+        return p.nega ? inv_dispatch<uint32_t, true>(p, p.a32, a, b, c, batch)
+                      : inv_dispatch<uint32_t, false>(p, p.a32, a, b, c, batch);
+    return p.nega ? inv_dispatch<uint64_t, true>(p, p.a64, a, b, c, batch)
+                  : inv_dispatch<uint64_t, false>(p, p.a64, a, b, c, batch);
+}
+
+hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch) {
+    return inv_any(p, in, nullptr, out, batch);
+}
+hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch) {
+    return inv_any(p, a, b, c, batch);
+}
+
+}  // namespace fhe

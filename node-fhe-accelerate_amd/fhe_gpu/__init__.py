@@ -1,0 +1,574 @@
+"""fhe_gpu -- Python host mirror of the reference operator interface over the
+MI355X C-ABI (``include/fhe_gpu.h``, ``build/libfhe_gpu.so``).
+
+Class and method names follow the reference C++ classes so parity tests read
+like the reference's own tests:
+
+=============================  ==============================================
+reference (cpp/include/...)    here
+=============================  ==============================================
+NTTProcessor                   :class:`NTTProcessor`   (ntt_processor.h:49-306)
+PolynomialRing                 :class:`PolynomialRing` (polynomial_ring.h:101-516)
+ModularArithmetic              :class:`ModularArithmetic` (modular_arithmetic.h:20-80;
+                               the N-API class of index.d.ts:32-44)
+BarrettReducer                 :class:`BarrettReducer` (modular_arithmetic.h:82-)
+MultiLimbModularArithmetic     :class:`MultiLimbModularArithmetic`
+BootstrapEngine::external_product  :class:`ExternalProduct`
+HardwareDetector::detect       :func:`detect_hardware`
+=============================  ==============================================
+
+Buffers: numpy ``uint64`` arrays (host; the call stages through HBM) or torch
+CUDA tensors of dtype int64/uint64 (device-resident; enqueued on the current
+torch stream, no host sync).  Shapes are ``[..., n]``: leading dims are the
+batch.  Errors raise :class:`FHEError` carrying the reference's exception text.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is present
+every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+try:  # share torch's HIP runtime when torch is present (one runtime per process)
+    import torch  # noqa: F401
+
+    _HAVE_TORCH = True
+except Exception:  # pragma: no cover
+    torch = None
+    _HAVE_TORCH = False
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_PKG)
+LIB_PATH = os.environ.get("FHE_GPU_LIB", os.path.join(_ROOT, "build", "libfhe_gpu.so"))
+
+FHE_OK = 0
+FHE_HOST, FHE_DEVICE = 0, 1
+MODE_COMPAT, MODE_NEGACYCLIC = 0, 1
+
+ERROR_NAMES = {
+    -1: "DEGREE_POW2", -2: "DEGREE_RANGE", -3: "MODULUS_EVEN", -4: "NOT_NTT_FRIENDLY",
+    -5: "COUNT", -6: "NO_ROOT", -7: "MONT_MODULUS", -8: "ZERO_MODULUS", -9: "INVALID_ARG",
+    -10: "UNSUPPORTED", -11: "DEVICE", -12: "OOM",
+}
+
+
+class FHEError(ValueError):
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+        self.name = ERROR_NAMES.get(code, "UNKNOWN")
+
+
+class HwCaps(C.Structure):
+    _fields_ = [
+        ("device_count", C.c_int32), ("compute_units", C.c_int32), ("wavefront_size", C.c_int32),
+        ("xcds", C.c_int32), ("hbm_bytes", C.c_uint64), ("lds_bytes_per_cu", C.c_uint64),
+        ("arch", C.c_char * 32), ("name", C.c_char * 96),
+    ]
+
+
+class CtxInfo(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32), ("log_n", C.c_uint32), ("q", C.c_uint64), ("psi", C.c_uint64),
+        ("psi_inv", C.c_uint64), ("inv_n", C.c_uint64), ("mode", C.c_int32), ("word_bits", C.c_int32),
+        ("device", C.c_int32), ("polys_per_block", C.c_int32), ("threads_per_block", C.c_int32),
+    ]
+
+
+u64p = C.POINTER(C.c_uint64)
+vp = C.c_void_p
+
+# (name, restype, argtypes) of every entry point declared in include/fhe_gpu.h
+SIGNATURES = [
+    ("fhe_last_error", C.c_char_p, []),
+    ("fhe_version", C.c_char_p, []),
+    ("fhe_detect", C.c_int, [C.POINTER(HwCaps)]),
+    ("fhe_ctx_create", C.c_int, [C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.POINTER(vp)]),
+    ("fhe_ctx_destroy", None, [vp]),
+    ("fhe_ctx_set_stream", C.c_int, [vp, vp]),
+    ("fhe_ctx_stream", vp, [vp]),
+    ("fhe_ctx_synchronize", C.c_int, [vp]),
+    ("fhe_ctx_get_info", C.c_int, [vp, C.POINTER(CtxInfo)]),
+    ("fhe_ctx_get_twiddles", C.c_int, [vp, vp, vp]),
+    ("fhe_ntt_fwd_batch", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_ntt_inv_batch", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_ntt_fwd_mul_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_polymul_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_pointwise_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_poly_add_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_poly_sub_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_poly_neg_batch", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_poly_mul_scalar_batch", C.c_int, [vp, vp, C.c_uint64, vp, C.c_size_t, C.c_int]),
+    ("fhe_ggsw_prepare", C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, C.c_int]),
+    ("fhe_external_product_batch", C.c_int,
+     [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_decompose_batch", C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_modmul_batch", C.c_int, [C.c_uint64, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
+    ("fhe_ml_constants", C.c_int, [u64p, u64p]),
+    ("fhe_ml_montmul_batch", C.c_int, [u64p, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
+    ("fhe_mont_constants_compat", C.c_int, [C.c_uint64, u64p]),
+    ("fhe_compat_montgomery_mul", C.c_uint64, [u64p, C.c_uint64, C.c_uint64]),
+    ("fhe_compat_to_montgomery", C.c_uint64, [u64p, C.c_uint64]),
+    ("fhe_compat_from_montgomery", C.c_uint64, [u64p, C.c_uint64]),
+    ("fhe_compat_mod_add", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("fhe_compat_mod_sub", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("fhe_dev_alloc", C.c_int, [C.c_int, C.c_size_t, C.POINTER(vp)]),
+    ("fhe_dev_free", C.c_int, [vp]),
+    ("fhe_memcpy_h2d", C.c_int, [vp, vp, C.c_size_t]),
+    ("fhe_memcpy_d2h", C.c_int, [vp, vp, C.c_size_t]),
+    ("fhe_device_synchronize", C.c_int, [C.c_int]),
+    ("fhe_event_create", C.c_int, [C.POINTER(vp)]),
+    ("fhe_event_destroy", C.c_int, [vp]),
+    ("fhe_event_record", C.c_int, [vp, vp]),
+    ("fhe_event_elapsed_ms", C.c_int, [vp, vp, C.POINTER(C.c_float)]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libfhe_gpu.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FHEError(-11, f"libfhe_gpu.so not found at {LIB_PATH}; run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != FHE_OK:
+        raise FHEError(rc, lib().fhe_last_error().decode(errors="replace"))
+
+
+def version() -> str:
+    return lib().fhe_version().decode()
+
+
+def detect_hardware() -> dict:
+    """HardwareDetector::detect() / N-API detectHardware() for the MI355X."""
+    caps = HwCaps()
+    _check(lib().fhe_detect(C.byref(caps)))
+    return {
+        "deviceCount": caps.device_count, "computeUnits": caps.compute_units,
+        "wavefrontSize": caps.wavefront_size, "xcds": caps.xcds, "hbmBytes": caps.hbm_bytes,
+        "ldsBytesPerCu": caps.lds_bytes_per_cu, "arch": caps.arch.decode(), "name": caps.name.decode(),
+    }
+
+
+# ----------------------------------------------------------------- buffers
+def _is_tensor(x) -> bool:
+    return _HAVE_TORCH and isinstance(x, torch.Tensor)
+
+
+def _stream_ptr():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class _Buf:
+    """Pointer + placement for one argument."""
+
+    __slots__ = ("ptr", "where", "count", "keep")
+
+    def __init__(self, x, writable=False):
+        if _is_tensor(x):
+            if not x.is_cuda:
+                raise FHEError(-9, "torch tensors must be on a GPU (use numpy arrays for host data)")
+            if x.dtype not in (torch.int64, torch.uint64):
+                raise FHEError(-9, "device buffers must be int64/uint64 tensors")
+            if not x.is_contiguous():
+                raise FHEError(-9, "device buffers must be contiguous")
+            self.ptr, self.where, self.count, self.keep = x.data_ptr(), FHE_DEVICE, x.numel(), x
+        else:
+            a = x
+            if not (isinstance(a, np.ndarray) and a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]):
+                if writable:
+                    raise FHEError(-9, "output must be a C-contiguous numpy uint64 array")
+                a = np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+            self.ptr, self.where, self.count, self.keep = a.ctypes.data, FHE_HOST, a.size, a
+
+
+def _where(*bufs: _Buf) -> int:
+    w = {b.where for b in bufs if b is not None}
+    if len(w) != 1:
+        raise FHEError(-9, "all buffers of one call must be host arrays or all device tensors")
+    return w.pop()
+
+
+def _like(x):
+    if _is_tensor(x):
+        return torch.empty_like(x)
+    return np.empty(np.shape(x), dtype=np.uint64)
+
+
+def _as_u64(x):
+    if _is_tensor(x):
+        return x
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+
+
+# ----------------------------------------------------------------- static helpers
+def is_power_of_two(n: int) -> bool:  # ntt_processor.cpp:25-27
+    return n > 0 and (n & (n - 1)) == 0
+
+
+def log2_pow2(n: int) -> int:  # :29-36
+    r = 0
+    while n > 1:
+        n >>= 1
+        r += 1
+    return r
+
+
+def bit_reverse(index: int, bits: int) -> int:  # :38-45
+    r = 0
+    for _ in range(bits):
+        r = (r << 1) | (index & 1)
+        index >>= 1
+    return r
+
+
+def mod_pow(base: int, exp: int, mod: int) -> int:  # :47-62
+    return pow(base % mod, exp, mod) if mod != 1 else 0
+
+
+def mod_inverse(a: int, m: int) -> int:  # :64-90 (signed extended Euclid)
+    if m == 0:
+        raise FHEError(-8, "Modulus cannot be zero")
+    if m == 1:
+        return 0
+    return pow(a % m, -1, m)
+
+
+def find_primitive_root(degree: int, modulus: int) -> int:  # :92-128
+    two_n = 2 * degree
+    if (modulus - 1) % two_n:
+        raise FHEError(-4, "Modulus is not NTT-friendly: q ≢ 1 (mod 2N)")
+    e = (modulus - 1) // two_n
+    for g in range(2, min(modulus, 1 << 22)):
+        w = pow(g, e, modulus)
+        if pow(w, two_n, modulus) == 1 and pow(w, degree, modulus) == modulus - 1:
+            return w
+    raise FHEError(-6, "Could not find primitive root for given parameters")
+
+
+# ----------------------------------------------------------------- NTT / ring
+class NTTProcessor:
+    """NTTProcessor(degree, modulus) on the MI355X (ntt_processor.h:49-306).
+
+    ``mode='compat'`` reproduces the reference transform bit for bit;
+    ``mode='negacyclic'`` is the psi-twisted transform whose pointwise product
+    is multiplication mod X^N + 1.
+    """
+
+    is_power_of_two = staticmethod(is_power_of_two)
+    log2_pow2 = staticmethod(log2_pow2)
+    bit_reverse = staticmethod(bit_reverse)
+    mod_pow = staticmethod(mod_pow)
+    mod_inverse = staticmethod(mod_inverse)
+    find_primitive_root = staticmethod(find_primitive_root)
+
+    def __init__(self, degree: int, modulus: int, mode: str = "compat", device: int = 0):
+        m = {"compat": MODE_COMPAT, "negacyclic": MODE_NEGACYCLIC}.get(mode)
+        if m is None:
+            raise FHEError(-9, f"unknown mode {mode!r}")
+        h = C.c_void_p()
+        _check(lib().fhe_ctx_create(degree, modulus, m, device, C.byref(h)))
+        self._h = h
+        self.degree, self.modulus, self.mode, self.device = degree, modulus, mode, device
+        info = CtxInfo()
+        _check(lib().fhe_ctx_get_info(h, C.byref(info)))
+        self.info = info
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.fhe_ctx_destroy(h)
+        self._h = None
+
+    __del__ = close
+
+    # -- introspection (get_degree/get_modulus/get_twiddles, ntt_processor.h)
+    def get_degree(self):
+        return self.degree
+
+    def get_modulus(self):
+        return self.modulus
+
+    @property
+    def primitive_root(self):
+        return self.info.psi
+
+    @property
+    def inv_n(self):
+        return self.info.inv_n
+
+    def get_twiddles(self):
+        f = np.empty(self.degree, dtype=np.uint64)
+        i = np.empty(self.degree, dtype=np.uint64)
+        _check(lib().fhe_ctx_get_twiddles(self._h, f.ctypes.data, i.ctypes.data))
+        return {"forward": f, "inverse": i, "primitive_root": self.info.psi, "inv_n": self.info.inv_n}
+
+    # -- plumbing
+    def _batch(self, x) -> int:
+        shape = tuple(x.shape)
+        if not shape or shape[-1] != self.degree:
+            raise FHEError(-5, "Coefficient count must equal polynomial degree")
+        b = 1
+        for s in shape[:-1]:
+            b *= s
+        return b
+
+    def _bind_stream(self, where):
+        if where == FHE_DEVICE:
+            _check(lib().fhe_ctx_set_stream(self._h, _stream_ptr()))
+
+    def _unary(self, fn, x, out):
+        x = _as_u64(x)
+        nb = self._batch(x)
+        out = _like(x) if out is None else out
+        bi, bo = _Buf(x), _Buf(out, True)
+        w = _where(bi, bo)
+        self._bind_stream(w)
+        _check(fn(self._h, bi.ptr, bo.ptr, nb, w))
+        return out
+
+    def _binary(self, fn, a, b, out):
+        a, b = _as_u64(a), _as_u64(b)
+        nb = self._batch(a)
+        if tuple(b.shape) != tuple(a.shape):
+            raise FHEError(-9, "operand shapes differ")
+        out = _like(a) if out is None else out
+        ba, bb, bo = _Buf(a), _Buf(b), _Buf(out, True)
+        w = _where(ba, bb, bo)
+        self._bind_stream(w)
+        _check(fn(self._h, ba.ptr, bb.ptr, bo.ptr, nb, w))
+        return out
+
+    # -- transforms
+    def forward_ntt(self, coeffs, out=None):
+        """forward_ntt (ntt_processor.cpp:262-319); pass out=coeffs for in place."""
+        return self._unary(lib().fhe_ntt_fwd_batch, coeffs, out)
+
+    def inverse_ntt(self, coeffs, out=None):
+        """inverse_ntt (ntt_processor.cpp:325-388)."""
+        return self._unary(lib().fhe_ntt_inv_batch, coeffs, out)
+
+    forward_ntt_batch = forward_ntt
+    inverse_ntt_batch = inverse_ntt
+
+    def forward_ntt_mul(self, coeffs, w, out=None):
+        """to_ntt(coeffs) then pointwise by w (config C3, fused)."""
+        return self._binary(lib().fhe_ntt_fwd_mul_batch, coeffs, w, out)
+
+
+class PolynomialRing(NTTProcessor):
+    """PolynomialRing(degree, modulus) (polynomial_ring.h:101-516) over batches."""
+
+    def multiply(self, a, b, out=None):
+        """multiply (polynomial_ring.cpp:421-447): inv(fwd(a) (.) fwd(b)), fused."""
+        return self._binary(lib().fhe_polymul_batch, a, b, out)
+
+    def pointwise_multiply(self, a, b, out=None):
+        return self._binary(lib().fhe_pointwise_batch, a, b, out)
+
+    def add(self, a, b, out=None):
+        return self._binary(lib().fhe_poly_add_batch, a, b, out)
+
+    def subtract(self, a, b, out=None):
+        return self._binary(lib().fhe_poly_sub_batch, a, b, out)
+
+    def negate(self, a, out=None):
+        return self._unary(lib().fhe_poly_neg_batch, a, out)
+
+    def multiply_scalar(self, a, scalar: int, out=None):
+        a = _as_u64(a)
+        nb = self._batch(a)
+        out = _like(a) if out is None else out
+        ba, bo = _Buf(a), _Buf(out, True)
+        w = _where(ba, bo)
+        self._bind_stream(w)
+        _check(lib().fhe_poly_mul_scalar_batch(self._h, ba.ptr, scalar, bo.ptr, nb, w))
+        return out
+
+    def to_ntt(self, p, out=None):
+        return self.forward_ntt(p, out)
+
+    def from_ntt(self, p, out=None):
+        return self.inverse_ntt(p, out)
+
+
+class ExternalProduct:
+    """BootstrapEngine::external_product (bootstrap_engine.cpp:431-518) for a
+    batch of GLWE ciphertexts ([..., k+1, n]) against one GGSW
+    ([(k+1)*level, k+1, n], coefficient form, reference row order)."""
+
+    def __init__(self, ring: NTTProcessor, ggsw, base_log: int, level: int, k: int = 1):
+        self.ring, self.base_log, self.level, self.k = ring, base_log, level, k
+        g = _as_u64(ggsw)
+        exp = ((k + 1) * level, k + 1, ring.degree)
+        if tuple(g.shape) != exp:
+            raise FHEError(-9, f"ggsw shape must be {exp}")
+        self.ggsw_ntt = _like(g)
+        bi, bo = _Buf(g), _Buf(self.ggsw_ntt, True)
+        w = _where(bi, bo)
+        ring._bind_stream(w)
+        _check(lib().fhe_ggsw_prepare(ring._h, k, level, bi.ptr, bo.ptr, w))
+
+    def __call__(self, glwe, out=None):
+        glwe = _as_u64(glwe)
+        shape = tuple(glwe.shape)
+        if len(shape) < 2 or shape[-2:] != (self.k + 1, self.ring.degree):
+            raise FHEError(-9, "glwe must have shape [..., k+1, n]")
+        nb = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+        out = _like(glwe) if out is None else out
+        bi, bk, bo = _Buf(glwe), _Buf(self.ggsw_ntt), _Buf(out, True)
+        w = _where(bi, bk, bo)
+        self.ring._bind_stream(w)
+        _check(lib().fhe_external_product_batch(self.ring._h, self.k, self.base_log, self.level, bi.ptr, bk.ptr,
+                                                bo.ptr, nb, w))
+        return out
+
+
+def decompose_polynomial(ring: NTTProcessor, poly, base_log: int, level: int, out=None):
+    """BootstrapEngine::decompose_polynomial (bootstrap_engine.cpp:152-185);
+    poly [..., n] -> [..., level, n]."""
+    poly = _as_u64(poly)
+    nb = ring._batch(poly)
+    if out is None:
+        shape = tuple(poly.shape[:-1]) + (level, ring.degree)
+        out = torch.empty(shape, dtype=poly.dtype, device=poly.device) if _is_tensor(poly) else np.empty(
+            shape, dtype=np.uint64)
+    bi, bo = _Buf(poly), _Buf(out, True)
+    w = _where(bi, bo)
+    ring._bind_stream(w)
+    _check(lib().fhe_decompose_batch(ring._h, base_log, level, bi.ptr, bo.ptr, nb, w))
+    return out
+
+
+# ----------------------------------------------------------------- modular arithmetic
+def modmul_batch(q: int, a, b, out=None, device: int = 0):
+    """BarrettReducer::barrett_mul contract, batched on the GPU: a*b mod q."""
+    a, b = _as_u64(a), _as_u64(b)
+    out = _like(a) if out is None else out
+    ba, bb, bo = _Buf(a), _Buf(b), _Buf(out, True)
+    if not (ba.count == bb.count == bo.count):
+        raise FHEError(-9, "operand sizes differ")
+    w = _where(ba, bb, bo)
+    s = _stream_ptr() if w == FHE_DEVICE else None
+    _check(lib().fhe_modmul_batch(q, ba.ptr, bb.ptr, bo.ptr, ba.count, w, device, s))
+    return out
+
+
+class BarrettReducer:
+    """BarrettReducer(modulus) (modular_arithmetic.cpp:238-280)."""
+
+    def __init__(self, modulus: int):
+        if modulus == 0:
+            raise FHEError(-8, "Modulus must be non-zero for Barrett reduction")
+        self.modulus = modulus
+
+    def barrett_mul_batch(self, a, b, out=None, device: int = 0):
+        return modmul_batch(self.modulus, a, b, out, device)
+
+    def barrett_mul(self, a: int, b: int) -> int:
+        return int(self.barrett_mul_batch(np.array([a], np.uint64), np.array([b], np.uint64))[0])
+
+
+class MultiLimbModularArithmetic:
+    """2-limb MultiLimbModularArithmetic (modular_arithmetic.cpp:471-693)."""
+
+    def __init__(self, modulus_limbs):
+        self.q = (C.c_uint64 * 2)(*[int(x) for x in modulus_limbs])
+        k = (C.c_uint64 * 7)()
+        _check(lib().fhe_ml_constants(self.q, k))
+        self.constants = list(k)
+
+    def montgomery_mul_batch(self, a, b, out=None, device: int = 0):
+        """a, b: [..., 2] little-endian limbs."""
+        a, b = _as_u64(a), _as_u64(b)
+        out = _like(a) if out is None else out
+        ba, bb, bo = _Buf(a), _Buf(b), _Buf(out, True)
+        if ba.count % 2 or not (ba.count == bb.count == bo.count):
+            raise FHEError(-9, "operands must be [..., 2] limb arrays of equal size")
+        w = _where(ba, bb, bo)
+        s = _stream_ptr() if w == FHE_DEVICE else None
+        _check(lib().fhe_ml_montmul_batch(self.q, ba.ptr, bb.ptr, bo.ptr, ba.count // 2, w, device, s))
+        return out
+
+
+class ModularArithmetic:
+    """The N-API ``ModularArithmetic`` class (index.d.ts:32-44,
+    src/native/lib.rs:42-121) with the reference's exact constants."""
+
+    def __init__(self, modulus: int):
+        if modulus <= 0:
+            raise FHEError(-9, "Modulus must be positive")
+        self._k = (C.c_uint64 * 4)()
+        _check(lib().fhe_mont_constants_compat(modulus, self._k))
+        self.modulus = modulus
+
+    @staticmethod
+    def _nn(*xs):
+        for x in xs:
+            if x < 0:
+                raise FHEError(-9, "Inputs must be non-negative")
+
+    def montgomery_mul(self, a, b):
+        self._nn(a, b)
+        return lib().fhe_compat_montgomery_mul(self._k, a, b)
+
+    def mod_add(self, a, b):
+        self._nn(a, b)
+        return lib().fhe_compat_mod_add(self.modulus, a, b)
+
+    def mod_sub(self, a, b):
+        self._nn(a, b)
+        return lib().fhe_compat_mod_sub(self.modulus, a, b)
+
+    def to_montgomery(self, a):
+        self._nn(a)
+        return lib().fhe_compat_to_montgomery(self._k, a)
+
+    def from_montgomery(self, a):
+        self._nn(a)
+        return lib().fhe_compat_from_montgomery(self._k, a)
+
+    def get_modulus(self):
+        return self.modulus
+
+    @property
+    def constants(self):
+        return list(self._k)
+
+
+# ----------------------------------------------------------------- timing helper
+class HipEvent:
+    """hipEvent on an explicit stream (for kernel timing in bench.py)."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().fhe_event_create(C.byref(h)))
+        self._h = h
+
+    def record(self, stream_ptr):
+        _check(lib().fhe_event_record(self._h, C.c_void_p(stream_ptr)))
+
+    def elapsed_ms(self, end: "HipEvent") -> float:
+        ms = C.c_float()
+        _check(lib().fhe_event_elapsed_ms(self._h, end._h, C.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.fhe_event_destroy(h)

@@ -1,0 +1,183 @@
+"""Generate the golden fixtures in tests/golden/ (committed; rerun to refresh).
+
+Provenance (see DESIGN.md "Oracle and pinning"):
+  * ``reference_kat.json`` -- known answers copied as DATA from the
+    reference's own tests (cpp/tests/test_ntt_processor.cpp:34-150,
+    cpp/tests/test_polynomial_ring.cpp:69-185) and the psi table of
+    SURVEY.md section 8 (values measured on the compiled reference when the
+    survey was written).
+  * every other file -- outputs of the C restatement ``oracle/ref_cpu.c``;
+    for sizes where it is feasible each vector is ALSO recomputed by the
+    independent big-integer restatement ``oracle/pyref.py`` (which follows
+    the reference's TypeScript restatement) and generation aborts on any
+    mismatch.  The reference C++ itself cannot be built in this image
+    (modular_arithmetic.h:5 includes <arm_neon.h>), so these are restatement
+    vectors, cross-checked, not reference-binary outputs.
+
+Inputs: TestRandom(seed) = std::mt19937_64 raw draws % q, exactly as the
+reference tests draw coefficients (cpp/tests/test_harness.h:29-73), and
+splitmix64(seed ^ index) % q for the larger sizes.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import oracle  # noqa: E402
+from oracle import pyref  # noqa: E402
+
+P27 = 132120577
+P62 = 4611686018326724609
+P40 = 1099511627777  # 2^40 + 1: not prime, the root search never ends (as in the reference)
+Q2048 = 40961  # 10*4096 + 1, prime
+
+SMALL = [(8, 17), (16, 97), (32, 193), (64, 257), (128, 769), (256, 7681), (512, 12289),
+         (1024, P27), (1024, P62), (2048, Q2048), (4096, P27)]
+LARGE = [(4096, P62), (16384, P27), (16384, P62)]
+
+
+def L(a):
+    return [int(x) for x in np.asarray(a).ravel()]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<u8").tobytes()).hexdigest()
+
+
+def dump(name, obj):
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(obj, f, separators=(",", ":"))
+    print("wrote", name)
+
+
+def reference_kat():
+    return {
+        "source": "cpp/tests/test_ntt_processor.cpp:34-150, cpp/tests/test_polynomial_ring.cpp:69-185, SURVEY.md 8",
+        "is_power_of_two_true": [1, 2, 4, 1024, 32768],
+        "is_power_of_two_false": [0, 3, 5, 1000],
+        "log2_pow2": [[1, 0], [2, 1], [4, 2], [1024, 10], [32768, 15]],
+        "bit_reverse_3": [[0, 0], [1, 4], [2, 2], [3, 6], [4, 1], [5, 5], [6, 3], [7, 7]],
+        "mod_pow": [[2, 10, 1000, 24], [3, 5, 7, 5], [123, 0, 1000, 1], [3, 16, 17, 1]],
+        "mod_inverse_products": [[3, 7], [12345, P27]],
+        "psi_table": [[1024, P27, 113022246], [4096, P27, 67542050], [16384, P27, 39393627],
+                      [16384, P62, 4096621604056103545]],
+        "ring_q17": {
+            "add": [[[1, 2, 3, 4, 5, 6, 7, 8], [8, 7, 6, 5, 4, 3, 2, 1], [9] * 8],
+                    [[10] * 8, [10] * 8, [3] * 8]],
+            "sub": [[[10] * 8, [3] * 8, [7] * 8]],
+        },
+        "round_trip_configs": [[8, 17, 100, 42], [16, 97, 100, 42], [1024, P27, 20, 42]],
+    }
+
+
+def ntt_small():
+    out = []
+    for n, q in SMALL:
+        t = oracle.NTT(n, q)
+        x = oracle.testrandom_coeffs(42, q, n)
+        y = oracle.testrandom_coeffs(43, q, n)
+        w = oracle.testrandom_coeffs(44, q, n)
+        f = t.forward(x)
+        i = t.inverse(x)
+        m = t.polymul(x, y)
+        fm = t.fwd_mul(x, w)
+        if n <= 1024:
+            xs, ys = L(x), L(y)
+            assert L(f) == pyref.forward(xs, q), (n, q)
+            assert L(i) == pyref.inverse(xs, q), (n, q)
+            assert L(m) == pyref.polymul(xs, ys, q), (n, q)
+        assert (t.inverse(f) == x).all()
+        out.append({"n": n, "q": q, "psi": t.psi, "x": L(x), "y": L(y), "w": L(w),
+                    "forward": L(f), "inverse": L(i), "polymul": L(m), "fwd_mul": L(fm)})
+    return out
+
+
+def ntt_large():
+    out = []
+    for n, q in LARGE:
+        t = oracle.NTT(n, q)
+        b = 4
+        x = oracle.splitmix_fill(0x5EED, q, b * n).reshape(b, n)
+        y = oracle.splitmix_fill(0xB0B, q, b * n).reshape(b, n)
+        f = t.forward(x)
+        i = t.inverse(x)
+        m = t.polymul(x, y)
+        fm = t.fwd_mul(x, y)
+        out.append({"n": n, "q": q, "batch": b, "seed_x": 0x5EED, "seed_y": 0xB0B,
+                    "sha_forward": sha(f), "sha_inverse": sha(i), "sha_polymul": sha(m), "sha_fwd_mul": sha(fm),
+                    "head_forward": L(f[0, :8]), "head_polymul": L(m[0, :8])})
+    return out
+
+
+def modmul():
+    rng = np.random.default_rng(7)
+    qs = [17, 97, P27, P40, P62, 3, 2 ** 61 - 1, 2 ** 63 + 29, 2 ** 64 - 59, 1000, 2 ** 62, 1]
+    out = []
+    for q in qs:
+        a = rng.integers(0, 2 ** 64 - 1, 64, dtype=np.uint64, endpoint=True)
+        b = rng.integers(0, 2 ** 64 - 1, 64, dtype=np.uint64, endpoint=True)
+        c = oracle.modmul_batch(q, a, b)
+        assert L(c) == [(int(u) * int(v)) % q for u, v in zip(a, b)]
+        out.append({"q": q, "a": L(a), "b": L(b), "c": L(c)})
+    return out
+
+
+def multi_limb():
+    rng = np.random.default_rng(11)
+    mods = [[P62, 1], [0xFFFFFFFFFFFFFFC5, 0xFFFFFFFFFFFFFFFF], [1, 1 << 63], [0x1234567890ABCDEF, 0x0FEDCBA987654321]]
+    out = []
+    for qm in mods:
+        k = oracle.ml_constants(qm)
+        qv = qm[0] | (qm[1] << 64)
+        a = rng.integers(0, 2 ** 64 - 1, (32, 2), dtype=np.uint64, endpoint=True)
+        b = rng.integers(0, 2 ** 64 - 1, (32, 2), dtype=np.uint64, endpoint=True)
+        # canonical operands (< q), as Montgomery arithmetic expects
+        for arr in (a, b):
+            for r in range(arr.shape[0]):
+                v = (int(arr[r, 0]) | (int(arr[r, 1]) << 64)) % qv
+                arr[r, 0], arr[r, 1] = v & (2 ** 64 - 1), v >> 64
+        c = oracle.ml_montmul_batch(qm, a, b)
+        out.append({"q": qm, "constants": k, "a": L(a), "b": L(b), "c": L(c)})
+    return out
+
+
+def extprod():
+    out = []
+    for n, q, bl, lv in [(64, 257, 3, 2), (256, 7681, 4, 3), (1024, P27, 9, 3), (1024, P62, 23, 1), (1024, P62, 15, 2)]:
+        t = oracle.NTT(n, q)
+        k = 1
+        glwe = oracle.testrandom_coeffs(5, q, (k + 1) * n).reshape(k + 1, n)
+        ggsw = oracle.testrandom_coeffs(6, q, (k + 1) * lv * (k + 1) * n).reshape((k + 1) * lv, k + 1, n)
+        res = t.external_product(k, bl, lv, glwe, ggsw)
+        out.append({"n": n, "q": q, "base_log": bl, "level": lv, "k": k, "glwe": L(glwe), "ggsw": L(ggsw),
+                    "out": L(res)})
+    return out
+
+
+def negacyclic():
+    out = []
+    for n, q in [(8, 17), (16, 97), (64, 257), (256, 7681)]:
+        x = L(oracle.testrandom_coeffs(1, q, n))
+        y = L(oracle.testrandom_coeffs(2, q, n))
+        prod = pyref.negacyclic_schoolbook(x, y, q)
+        fx = pyref.negacyclic_forward(x, q)
+        assert pyref.negacyclic_inverse(fx, q) == x
+        assert pyref.negacyclic_inverse([(a * b) % q for a, b in zip(fx, pyref.negacyclic_forward(y, q))], q) == prod
+        out.append({"n": n, "q": q, "x": x, "y": y, "forward": fx, "product": prod})
+    return out
+
+
+if __name__ == "__main__":
+    dump("reference_kat.json", reference_kat())
+    dump("ntt_small.json", ntt_small())
+    dump("ntt_large.json", ntt_large())
+    dump("modmul.json", modmul())
+    dump("multi_limb.json", multi_limb())
+    dump("extprod.json", extprod())
+    dump("negacyclic.json", negacyclic())

@@ -1,0 +1,244 @@
+"""Pin the CPU oracle (oracle/ref_cpu.c) before trusting it.
+
+1. The reference's own known-answer tests and properties
+   (cpp/tests/test_ntt_processor.cpp, test_polynomial_ring.cpp,
+   test_multi_limb.cpp) pass on the restatement.
+2. The psi table measured on the compiled reference.
+3. An independent big-integer restatement (oracle/pyref.py, following the
+   reference's TypeScript restatement) agrees bit for bit.
+4. The committed golden fixtures regenerate identically.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import pyref
+
+P27 = 132120577
+P62 = 4611686018326724609
+
+
+@pytest.fixture(scope="module")
+def kat(golden_dir):
+    with open(os.path.join(golden_dir, "reference_kat.json")) as f:
+        return json.load(f)
+
+
+def load(golden_dir, name):
+    with open(os.path.join(golden_dir, name)) as f:
+        return json.load(f)
+
+
+def U(x):
+    return np.array(x, dtype=np.uint64)
+
+
+# --------------------------------------------------- reference known answers
+def test_static_helpers(kat):
+    for n in kat["is_power_of_two_true"]:
+        assert oracle.is_power_of_two(n)
+    for n in kat["is_power_of_two_false"]:
+        assert not oracle.is_power_of_two(n)
+    for n, l in kat["log2_pow2"]:
+        assert oracle.log2_pow2(n) == l
+    for i, r in kat["bit_reverse_3"]:
+        assert oracle.bit_reverse(i, 3) == r
+    for b, e, m, r in kat["mod_pow"]:
+        assert oracle.mod_pow(b, e, m) == r
+    for a, m in kat["mod_inverse_products"]:
+        assert (a * oracle.mod_inverse(a, m)) % m == 1
+
+
+def test_psi_table_matches_compiled_reference(kat):
+    for n, q, psi in kat["psi_table"]:
+        t = oracle.NTT(n, q)
+        assert t.psi == psi
+        assert oracle.mod_pow(psi, 2 * n, q) == 1 and oracle.mod_pow(psi, n, q) == q - 1
+
+
+def test_constructor_errors():
+    with pytest.raises(oracle.OracleError, match="power of 2"):
+        oracle.NTT(12, 97)
+    with pytest.raises(oracle.OracleError, match="between 4 and 65536"):
+        oracle.NTT(2, 97)
+    with pytest.raises(oracle.OracleError, match="odd"):
+        oracle.NTT(8, 96)
+    with pytest.raises(oracle.OracleError, match="NTT-friendly"):
+        oracle.NTT(16, 17)
+
+
+def test_ntt_simple_q17():  # test_ntt_processor.cpp:152-179
+    t = oracle.NTT(8, 17)
+    x = U([1, 2, 3, 4, 5, 6, 7, 8])
+    assert (t.inverse(t.forward(x)) == x).all()
+
+
+def test_round_trip_property(kat):  # test_ntt_processor.cpp:193-268, seed 42 draw order
+    for n, q, iters, seed in kat["round_trip_configs"]:
+        t = oracle.NTT(n, q)
+        draws = oracle.testrandom_coeffs(seed, q, n * iters).reshape(iters, n)
+        assert (t.inverse(t.forward(draws)) == draws).all()
+
+
+def test_transforms_data():  # test_ntt_processor.cpp:327-356
+    t = oracle.NTT(1024, P27)
+    x = oracle.testrandom_coeffs(42, P27, 1024)
+    assert int((t.forward(x) != x).sum()) > 100
+
+
+def test_ring_q17(kat):  # test_polynomial_ring.cpp:69-185
+    for a, b, c in kat["ring_q17"]["add"]:
+        assert list(oracle.poly_add(17, U(a), U(b))) == c
+    for a, b, c in kat["ring_q17"]["sub"]:
+        assert list(oracle.poly_sub(17, U(a), U(b))) == c
+    a = U([0, 1, 5, 16])
+    assert list(oracle.poly_neg(17, a)) == [0, 16, 12, 1]
+
+
+def test_polymul_identity_zero():  # test_polynomial_ring.cpp:191-219
+    t = oracle.NTT(64, 257)
+    x = oracle.testrandom_coeffs(3, 257, 64)
+    one = np.zeros(64, np.uint64)
+    one[0] = 1
+    # the compat transform is not the ring product, but fwd(1) is all ones
+    assert (t.forward(one) == 1).all()
+    assert (t.polymul(x, one) == x).all()
+    assert (t.polymul(x, np.zeros(64, np.uint64)) == 0).all()
+
+
+def test_multi_limb_round_trip():  # test_multi_limb.cpp:16-208 (Montgomery round trip)
+    for qm in ([P62, 1], [0x1234567890ABCDEF, 0x0FEDCBA987654321]):
+        k = oracle.ml_constants(qm)
+        qv = qm[0] | (qm[1] << 64)
+        R = 1 << 128
+        assert (k[2] | (k[3] << 64)) == R % qv
+        assert (k[4] | (k[5] << 64)) == (R * R) % qv
+        assert (k[6] * qm[0]) % (1 << 64) == (1 << 64) - 1  # -q^-1 mod 2^64
+        rng = np.random.default_rng(1)
+        for _ in range(50):
+            v = int(rng.integers(0, 2 ** 63)) * int(rng.integers(1, 2 ** 62)) % qv
+            a = U([[v & (2 ** 64 - 1), v >> 64]])
+            r2 = U([[k[4], k[5]]])
+            am = oracle.ml_montmul_batch(qm, a, r2)  # to_montgomery
+            one = U([[1, 0]])
+            back = oracle.ml_montmul_batch(qm, am, one)  # from_montgomery
+            assert int(back[0, 0]) | (int(back[0, 1]) << 64) == v
+
+
+def test_barrett_is_exact():  # barrett_mul correct
+    rng = np.random.default_rng(3)
+    for q in (P27, P62, 17, 2 ** 63 + 29):
+        a = rng.integers(0, 2 ** 64 - 1, 2000, dtype=np.uint64, endpoint=True)
+        b = rng.integers(0, 2 ** 64 - 1, 2000, dtype=np.uint64, endpoint=True)
+        c = oracle.modmul_batch(q, a, b)
+        assert [int(x) for x in c] == [int(x) * int(y) % q for x, y in zip(a, b)]
+
+
+def test_compat_montgomery_is_reference_quirk():  # 0/10000 correct
+    k = oracle.mont_constants(P27)
+    rng = np.random.default_rng(5)
+    ok = 0
+    for _ in range(2000):
+        a, b = int(rng.integers(0, P27)), int(rng.integers(0, P27))
+        r = oracle.from_mont(k, oracle.mont_mul(k, oracle.to_mont(k, a), oracle.to_mont(k, b)))
+        ok += r == a * b % P27
+    assert ok == 0
+    assert k[1] == (1 << 64) % P27 and k[2] == ((1 << 64) % P27) ** 2 % P27
+
+
+def test_mt19937_64_known_value():
+    # std::mt19937_64 default seed 5489: 10000th output (C++11 [rand.predef])
+    assert int(oracle.mt19937_64_raw(5489, 10000)[-1]) == 9981545732273789042
+
+
+# --------------------------------------------------- independent restatement
+@pytest.mark.parametrize("n,q", [(8, 17), (16, 97), (32, 193), (256, 7681), (512, 12289), (1024, P27), (1024, P62)])
+def test_oracle_matches_pyref(n, q):
+    t = oracle.NTT(n, q)
+    x = oracle.testrandom_coeffs(9, q, n)
+    y = oracle.testrandom_coeffs(10, q, n)
+    xs, ys = [int(v) for v in x], [int(v) for v in y]
+    assert [int(v) for v in t.forward(x)] == pyref.forward(xs, q)
+    assert [int(v) for v in t.inverse(x)] == pyref.inverse(xs, q)
+    assert [int(v) for v in t.polymul(x, y)] == pyref.polymul(xs, ys, q)
+
+
+def test_non_canonical_inputs_behave_mod_q():
+    t = oracle.NTT(64, 257)
+    x = np.random.default_rng(2).integers(0, 2 ** 64 - 1, 64, dtype=np.uint64, endpoint=True)
+    assert (t.forward(x) == t.forward(x % np.uint64(257))).all()
+    assert (t.inverse(x) == t.inverse(x % np.uint64(257))).all()
+
+
+def test_negacyclic_pyref_is_ring_product(golden_dir):
+    for case in load(golden_dir, "negacyclic.json"):
+        q = case["q"]
+        fx = pyref.negacyclic_forward(case["x"], q)
+        fy = pyref.negacyclic_forward(case["y"], q)
+        assert pyref.negacyclic_inverse([(a * b) % q for a, b in zip(fx, fy)], q) == case["product"]
+        assert case["product"] == pyref.negacyclic_schoolbook(case["x"], case["y"], q)
+
+
+# --------------------------------------------------- fixtures regenerate
+def test_golden_ntt_small(golden_dir):
+    for c in load(golden_dir, "ntt_small.json"):
+        t = oracle.NTT(c["n"], c["q"])
+        assert t.psi == c["psi"]
+        x, y, w = U(c["x"]), U(c["y"]), U(c["w"])
+        assert [int(v) for v in t.forward(x)] == c["forward"]
+        assert [int(v) for v in t.inverse(x)] == c["inverse"]
+        assert [int(v) for v in t.polymul(x, y)] == c["polymul"]
+        assert [int(v) for v in t.fwd_mul(x, w)] == c["fwd_mul"]
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<u8").tobytes()).hexdigest()
+
+
+def test_golden_ntt_large(golden_dir):
+    for c in load(golden_dir, "ntt_large.json"):
+        n, q, b = c["n"], c["q"], c["batch"]
+        t = oracle.NTT(n, q)
+        x = oracle.splitmix_fill(c["seed_x"], q, b * n).reshape(b, n)
+        y = oracle.splitmix_fill(c["seed_y"], q, b * n).reshape(b, n)
+        assert _sha(t.forward(x)) == c["sha_forward"]
+        assert _sha(t.polymul(x, y)) == c["sha_polymul"]
+
+
+def test_golden_extprod_and_ml(golden_dir):
+    for c in load(golden_dir, "extprod.json"):
+        t = oracle.NTT(c["n"], c["q"])
+        k, lv, n = c["k"], c["level"], c["n"]
+        glwe = U(c["glwe"]).reshape(k + 1, n)
+        ggsw = U(c["ggsw"]).reshape((k + 1) * lv, k + 1, n)
+        assert [int(v) for v in t.external_product(k, c["base_log"], lv, glwe, ggsw).ravel()] == c["out"]
+    for c in load(golden_dir, "multi_limb.json"):
+        assert oracle.ml_constants(c["q"]) == c["constants"]
+        a, b = U(c["a"]).reshape(-1, 2), U(c["b"]).reshape(-1, 2)
+        assert [int(v) for v in oracle.ml_montmul_batch(c["q"], a, b).ravel()] == c["c"]
+    for c in load(golden_dir, "modmul.json"):
+        assert [int(v) for v in oracle.modmul_batch(c["q"], U(c["a"]), U(c["b"]))] == c["c"]
+
+
+def test_external_product_equals_ntt_domain_accumulation(golden_dir):
+    """The linearity the GPU kernel relies on: sum_r inv(X_r) == inv(sum_r X_r)."""
+    c = load(golden_dir, "extprod.json")[2]
+    q, n, k, lv, bl = c["q"], c["n"], c["k"], c["level"], c["base_log"]
+    t = oracle.NTT(n, q)
+    glwe = U(c["glwe"]).reshape(k + 1, n)
+    ggsw = U(c["ggsw"]).reshape((k + 1) * lv, k + 1, n)
+    acc = [0] * (k + 1)
+    rows = []
+    for i in range(k + 1):
+        for d in oracle.decompose(q, glwe[i], bl, lv):
+            rows.append(t.forward(d))
+    for j in range(k + 1):
+        s = np.zeros(n, dtype=object)
+        for r, fd in enumerate(rows):
+            s = (s + oracle.pointwise(q, fd, t.forward(ggsw[r, j])).astype(object)) % q
+        acc[j] = t.inverse(U(list(s)))
+    assert [int(v) for v in np.concatenate(acc)] == c["out"]
