@@ -85,8 +85,10 @@ int fhe_detect(fhe_hw_caps *caps);
  * device: HIP device ordinal.                                              */
 int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out);
 void fhe_ctx_destroy(fhe_ctx *ctx);
-/* Use an existing hipStream_t (e.g. a torch stream) for FHE_DEVICE calls;
- * NULL restores the context's own stream. */
+/* Enqueue all later work of this context on the given hipStream_t (e.g. the
+ * caller's torch stream).  NULL selects the null (legacy default) stream,
+ * which is torch's default stream.  A new context uses a private
+ * non-blocking stream until this is called. */
 int fhe_ctx_set_stream(fhe_ctx *ctx, void *hip_stream);
 void *fhe_ctx_stream(const fhe_ctx *ctx);
 int fhe_ctx_synchronize(fhe_ctx *ctx);

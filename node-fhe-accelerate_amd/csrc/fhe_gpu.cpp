@@ -355,7 +355,7 @@ void fhe_ctx_destroy(fhe_ctx *c) {
 
 int fhe_ctx_set_stream(fhe_ctx *c, void *s) {
     if (int rc = check_ctx(c)) return rc;
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = (hipStream_t)s;  // NULL is the device's null (legacy default) stream
     c->plan.stream = c->stream;
     return FHE_OK;
 }

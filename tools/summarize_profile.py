@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Summarize a rocprofv3 run of tools/gpu_profile.sh into profiles/<tag>/.
+
+Per kernel of interest: average duration (kernel trace stats), and per
+launch the PMC counters.  HBM traffic per launch follows
+/opt/skills/guides/MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE come
+from separate --pmc passes, are in KiB, and on gfx950 FETCH_SIZE reports half
+the bytes of a wide coalesced streaming read, so
+    traffic_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+Only launches of the full benchmark batch are used (the bench's 2-row parity
+spot check is excluded by grid size).
+
+usage: summarize_profile.py gpurun_out/prof_<tag> profiles/<tag> [--kernel-substr fwd_mul]
+       [--workload kernel,n,batch,q]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    ksub = sys.argv[sys.argv.index("--kernel-substr") + 1] if "--kernel-substr" in sys.argv else "fwd_mul"
+    os.makedirs(dst, exist_ok=True)
+    out = {"source": src, "kernel_substr": ksub}
+    if "--workload" in sys.argv:
+        k, n, b, q = sys.argv[sys.argv.index("--workload") + 1].split(",")
+        out["workload"] = {"kernel": k, "n": int(n), "batch": int(b), "q": int(q)}
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+        rows = list(csv.DictReader(open(stats[0])))
+        out["kernel_stats"] = [
+            {k: (r[k][:160] if k == "Name" else r[k]) for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
+            for r in rows[:8]
+        ]
+    per_counter = defaultdict(list)
+    grid = {}
+    for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
+        acc = defaultdict(float)
+        names = {}
+        for r in csv.DictReader(open(f)):
+            if ksub not in r["Kernel_Name"]:
+                continue
+            key = (r["Dispatch_Id"], r["Counter_Name"])
+            acc[key] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"]
+            grid[r["Dispatch_Id"]] = int(r["Grid_Size"])
+            out["vgpr"] = r.get("VGPR_Count")
+            out["lds_bytes"] = r.get("LDS_Block_Size")
+            out["kernel_name"] = r["Kernel_Name"]
+        if not acc:
+            continue
+        gmax = max(grid.values())
+        for (d, c), v in acc.items():
+            if grid[d] == gmax:
+                per_counter[c].append(v)
+    pmc = {c: sum(v) / len(v) for c, v in per_counter.items()}
+    out["pmc_per_launch_avg"] = pmc
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        out["hbm_traffic_bytes_per_launch"] = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
+        out["traffic_note"] = "(2*FETCH_SIZE + WRITE_SIZE) KiB; gfx950 FETCH_SIZE counts half of wide streaming reads"
+    if "SQ_WAVE_CYCLES" in pmc:
+        w = pmc["SQ_WAVE_CYCLES"]
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if c in pmc:
+                out[c + "_frac_of_wave_cycles"] = pmc[c] / w
+    if "SQ_WAVES" in pmc and "SQ_INSTS_VALU" in pmc:
+        out["valu_insts_per_wave"] = pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]
+    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
