@@ -16,7 +16,7 @@
 // All are HBM-bound: 16-byte (2 x u64) loads/stores per lane, grid-stride.
 #include "fhe_internal.hpp"
 
-namespace fhe {
+namespace FHE_NS {
 
 static constexpr int kBlock = 256;
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -259,4 +259,4 @@ hipError_t launch_decompose(const ModConsts &m, const uint64_t *poly, uint64_t *
     return hipGetLastError();
 }
 
-}  // namespace fhe
+}  // namespace FHE_NS

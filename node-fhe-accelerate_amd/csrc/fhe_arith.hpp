@@ -11,10 +11,14 @@
 // to the reference's "%"-based arithmetic (ntt_processor.cpp:298-307,
 // polynomial_ring.cpp:512-526) even though the operation sequence differs.
 #pragma once
+// Kernel namespace; lab A/B builds override it so variants can share a process.
+#ifndef FHE_NS
+#define FHE_NS fhe
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-namespace fhe {
+namespace FHE_NS {
 
 __device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
 __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
@@ -57,6 +61,13 @@ struct Arith {
         x = a + b;
         y = a - b + q2;
     }
+    // Forward butterfly without reducing x: outputs grow by 2q per stage.
+    __device__ __forceinline__ void ct_lazy(W &x, W &y, Tw<W> t) const {
+        W b = shoup(y, t);
+        W a = x;
+        x = a + b;
+        y = a - b + q2;
+    }
     // Gentleman-Sande butterfly, values in [0, 2q).
     __device__ __forceinline__ void gs(W &x, W &y, Tw<W> t) const {
         W s = x + y;
@@ -88,4 +99,4 @@ __device__ __forceinline__ W load_lazy(uint64_t x, uint64_t lim, uint64_t q, uin
     return W(x);
 }
 
-}  // namespace fhe
+}  // namespace FHE_NS

@@ -71,9 +71,9 @@ W neg_inv_pow2(W q) {  // -q^-1 mod 2^W (q odd), Newton
     return W(0) - x;
 }
 template <typename W>
-fhe::Tw<W> make_tw(u64 w, u64 q) {
+FHE_NS::Tw<W> make_tw(u64 w, u64 q) {
     constexpr int BITS = sizeof(W) * 8;
-    fhe::Tw<W> t;
+    FHE_NS::Tw<W> t;
     t.w = (W)w;
     t.wp = (W)(((u128)w << BITS) / q);
     return t;
@@ -92,7 +92,7 @@ struct fhe_ctx {
     int mode = 0, device = 0, word = 64;
     hipStream_t own_stream = nullptr, stream = nullptr;
     Tables tab;
-    fhe::Plan plan{};
+    FHE_NS::Plan plan{};
     std::vector<u64> fwd_tw, inv_tw;  // reference twiddle vectors (host copy)
     std::mutex scratch_mu;
     void *scratch[3] = {nullptr, nullptr, nullptr};
@@ -132,11 +132,11 @@ int find_psi(u32 n, u64 q, u64 &psi) {
 }
 
 template <typename W>
-int build_tables(fhe_ctx *c, fhe::NttArgs<W> &A) {
+int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
     const u32 n = c->n, L = c->logn;
     const u64 q = c->q;
     constexpr int BITS = sizeof(W) * 8;
-    std::vector<fhe::Tw<W>> twf(n), twi(n), twist(n), untw(n), untw_r(n);
+    std::vector<FHE_NS::Tw<W>> twf(n), twi(n), twist(n), untw(n), untw_r(n);
     // stage-major: entry 2^s + j holds the twiddle of butterfly j in stage s
     for (u32 s = 0; s < L; ++s) {
         for (u32 j = 0; j < (1u << s); ++j) {
@@ -156,18 +156,18 @@ int build_tables(fhe_ctx *c, fhe::NttArgs<W> &A) {
         untw[i] = make_tw<W>(u, q);
         untw_r[i] = make_tw<W>(mulmod(u, R, q), q);
     }
-    const size_t bytes = sizeof(fhe::Tw<W>) * n;
+    const size_t bytes = sizeof(FHE_NS::Tw<W>) * n;
     void **dst[5] = {&c->tab.twf, &c->tab.twi, &c->tab.twist, &c->tab.untwist, &c->tab.untwist_r};
     const void *srcs[5] = {twf.data(), twi.data(), twist.data(), untw.data(), untw_r.data()};
     for (int i = 0; i < 5; ++i) {
         HIP_TRY(hipMalloc(dst[i], bytes), "hipMalloc(twiddles)");
         HIP_TRY(hipMemcpy(*dst[i], srcs[i], bytes, hipMemcpyHostToDevice), "hipMemcpy(twiddles)");
     }
-    A.twf = (const fhe::Tw<W> *)c->tab.twf;
-    A.twi = (const fhe::Tw<W> *)c->tab.twi;
-    A.twist = (const fhe::Tw<W> *)c->tab.twist;
-    A.untwist = (const fhe::Tw<W> *)c->tab.untwist;
-    A.untwist_r = (const fhe::Tw<W> *)c->tab.untwist_r;
+    A.twf = (const FHE_NS::Tw<W> *)c->tab.twf;
+    A.twi = (const FHE_NS::Tw<W> *)c->tab.twi;
+    A.twist = (const FHE_NS::Tw<W> *)c->tab.twist;
+    A.untwist = (const FHE_NS::Tw<W> *)c->tab.untwist;
+    A.untwist_r = (const FHE_NS::Tw<W> *)c->tab.untwist_r;
     A.ar.q = (W)q;
     A.ar.q2 = (W)(2 * q);
     A.ar.qinv = neg_inv_pow2<W>((W)q);
@@ -177,6 +177,7 @@ int build_tables(fhe_ctx *c, fhe::NttArgs<W> &A) {
     A.ninv = make_tw<W>(c->inv_n, q);
     A.ninv_r = make_tw<W>(ninv_r, q);
     A.rmod = make_tw<W>(R, q);
+    A.one = make_tw<W>(1, q);
     return FHE_OK;
 }
 
@@ -189,8 +190,8 @@ void free_tables(fhe_ctx *c) {
         if (s) { (void)hipFree(s); s = nullptr; }
 }
 
-fhe::ModConsts mod_consts(u64 q) {
-    fhe::ModConsts m{};
+FHE_NS::ModConsts mod_consts(u64 q) {
+    FHE_NS::ModConsts m{};
     m.q = q;
     m.mu = q > 1 ? (u64)((((u128)1) << 64) / q) : 0;
     m.fast = (q & 1) && q > 1 && !(q >> 63);
@@ -302,7 +303,7 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     if (int rc = find_psi(n, q, psi)) return rc;
     u32 logn = 0;
     while ((1u << logn) < n) ++logn;
-    if ((int)logn > fhe::kMaxLogN)
+    if ((int)logn > FHE_NS::kMaxLogN)
         return fail(FHE_ERR_UNSUPPORTED, "GPU kernels implement degrees up to 16384 (got " + std::to_string(n) + ")");
     if (q >> 62) return fail(FHE_ERR_UNSUPPORTED, "GPU kernels implement moduli below 2^62");
     int count = 0;
@@ -339,6 +340,7 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     c->plan.logn = logn;
     c->plan.word = c->word;
     c->plan.nega = mode;
+    c->plan.lazy = c->word == 32 && (u128)(4 + 2 * logn) * q <= ((u128)1 << 32);
     c->plan.stream = c->stream;
     *out = c;
     return FHE_OK;
@@ -389,65 +391,65 @@ int fhe_ctx_get_twiddles(const fhe_ctx *c, uint64_t *fwd, uint64_t *inv) {
 int fhe_ntt_fwd_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return fhe::launch_fwd(c->plan, d[0], o, nb, 0); });
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 0); });
 }
 int fhe_ntt_inv_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return fhe::launch_inv(c->plan, d[0], o, nb); });
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_inv(c->plan, d[0], o, nb); });
 }
 int fhe_ntt_fwd_mul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     if (!w && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     return run_poly_op(c, a, w, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_fwd_mul(c->plan, d[0], d[1], o, nb);
+        return FHE_NS::launch_fwd_mul(c->plan, d[0], d[1], o, nb);
     });
 }
 int fhe_polymul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_polymul(c->plan, d[0], d[1], o, nb);
+        return FHE_NS::launch_polymul(c->plan, d[0], d[1], o, nb);
     });
 }
 int fhe_pointwise_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
-    const fhe::ModConsts m = mod_consts(c->q);
+    const FHE_NS::ModConsts m = mod_consts(c->q);
     return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_modmul(m, d[0], d[1], o, nb * c->n, c->stream);
+        return FHE_NS::launch_modmul(m, d[0], d[1], o, nb * c->n, c->stream);
     });
 }
 int fhe_poly_add_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
-    const fhe::ModConsts m = mod_consts(c->q);
+    const FHE_NS::ModConsts m = mod_consts(c->q);
     return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_addsub(m, d[0], d[1], o, nb * c->n, 0, c->stream);
+        return FHE_NS::launch_addsub(m, d[0], d[1], o, nb * c->n, 0, c->stream);
     });
 }
 int fhe_poly_sub_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
-    const fhe::ModConsts m = mod_consts(c->q);
+    const FHE_NS::ModConsts m = mod_consts(c->q);
     return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_addsub(m, d[0], d[1], o, nb * c->n, 1, c->stream);
+        return FHE_NS::launch_addsub(m, d[0], d[1], o, nb * c->n, 1, c->stream);
     });
 }
 int fhe_poly_neg_batch(fhe_ctx *c, const uint64_t *a, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_neg(c->q, d[0], o, nb * c->n, c->stream);
+        return FHE_NS::launch_neg(c->q, d[0], o, nb * c->n, c->stream);
     });
 }
 int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, uint64_t *out, size_t batch,
                               int where) {
     if (int rc = check_ctx(c)) return rc;
-    const fhe::ModConsts m = mod_consts(c->q);
+    const FHE_NS::ModConsts m = mod_consts(c->q);
     const u64 s = scalar % c->q;
     const u64 sp = (u64)(((u128)s << 64) / c->q);
     return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_mul_scalar(m, d[0], s, sp, o, nb * c->n, c->stream);
+        return FHE_NS::launch_mul_scalar(m, d[0], s, sp, o, nb * c->n, c->stream);
     });
 }
 
@@ -464,7 +466,7 @@ int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggs
     if (level == 0) return fail(FHE_ERR_INVALID_ARG, "level must be >= 1");
     const size_t polys = (size_t)(k + 1) * level * (k + 1);
     return run_poly_op(c, ggsw, nullptr, ggsw_ntt, polys, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return fhe::launch_fwd(c->plan, d[0], o, nb, 1); });
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 1); });
 }
 
 int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
@@ -483,13 +485,13 @@ int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32
         int rc = e != hipSuccess ? hip_fail(e, "hipMemcpy(ggsw)") : FHE_OK;
         if (rc == FHE_OK)
             rc = run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb) {
-                return fhe::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], (const u64 *)dk, o, nb);
+                return FHE_NS::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], (const u64 *)dk, o, nb);
             });
         (void)hipFree(dk);
         return rc;
     }
     return run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return fhe::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], ggsw_ntt, o, nb);
+        return FHE_NS::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], ggsw_ntt, o, nb);
     });
 }
 
@@ -498,10 +500,10 @@ int fhe_decompose_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uin
     if (int rc = check_ctx(c)) return rc;
     if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
         return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
-    const fhe::ModConsts m = mod_consts(c->q);
+    const FHE_NS::ModConsts m = mod_consts(c->q);
     return run_poly_op(c, poly, nullptr, out, npoly, where, c->n, (size_t)c->n * level,
                        [&](const u64 *const *d, u64 *o, size_t nb) {
-                           return fhe::launch_decompose(m, d[0], o, c->n, nb, base_log, level, c->stream);
+                           return FHE_NS::launch_decompose(m, d[0], o, c->n, nb, base_log, level, c->stream);
                        });
 }
 
@@ -538,12 +540,12 @@ static int run_flat(int device, void *stream, int where, const u64 *a, const u64
 }
 
 static hipError_t modmul_thunk(const void *arg, const u64 *a, const u64 *b, u64 *c, size_t n, hipStream_t s) {
-    return fhe::launch_modmul(*(const fhe::ModConsts *)arg, a, b, c, n, s);
+    return FHE_NS::launch_modmul(*(const FHE_NS::ModConsts *)arg, a, b, c, n, s);
 }
 int fhe_modmul_batch(uint64_t q, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t count, int where,
                      int device, void *stream) {
     if (q == 0) return fail(FHE_ERR_ZERO_MODULUS, "Modulus must be non-zero for Barrett reduction");
-    const fhe::ModConsts m = mod_consts(q);
+    const FHE_NS::ModConsts m = mod_consts(q);
     return run_flat(device, stream, where, a, b, c, count, 1, modmul_thunk, &m);
 }
 
@@ -616,7 +618,7 @@ int fhe_ml_constants(const uint64_t q[2], uint64_t out[7]) {
 }
 
 static hipError_t ml_thunk(const void *arg, const u64 *a, const u64 *b, u64 *c, size_t n, hipStream_t s) {
-    return fhe::launch_ml_montmul((const u64 *)arg, a, b, c, n, s);
+    return FHE_NS::launch_ml_montmul((const u64 *)arg, a, b, c, n, s);
 }
 int fhe_ml_montmul_batch(const uint64_t q[2], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t count,
                          int where, int device, void *stream) {

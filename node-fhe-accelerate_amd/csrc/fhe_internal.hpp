@@ -7,12 +7,13 @@
 
 #include "ntt_core.hpp"
 
-namespace fhe {
+namespace FHE_NS {
 
 struct Plan {
     uint32_t logn;
     int word;   // 32 or 64
     int nega;   // 0 = compat, 1 = negacyclic
+    int lazy;   // 32-bit path with (4 + 2L) q <= 2^32: forward stages skip reductions
     hipStream_t stream;
     NttArgs<uint32_t> a32;
     NttArgs<uint64_t> a64;
@@ -50,4 +51,4 @@ hipError_t launch_ml_montmul(const uint64_t consts[7], const uint64_t *a, const 
 hipError_t launch_decompose(const ModConsts &m, const uint64_t *poly, uint64_t *out, uint32_t n, size_t npoly,
                             uint32_t base_log, uint32_t level, hipStream_t s);
 
-}  // namespace fhe
+}  // namespace FHE_NS

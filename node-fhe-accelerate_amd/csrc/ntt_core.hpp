@@ -22,7 +22,7 @@
 #pragma once
 #include "fhe_arith.hpp"
 
-namespace fhe {
+namespace FHE_NS {
 
 // ---------------------------------------------------------------- geometry
 template <int LOGN>
@@ -37,6 +37,21 @@ struct Geo {
     static constexpr int P = T >= 256 ? 1 : 256 / T;  // polynomials per workgroup
     static constexpr int THREADS = T * P;
     static constexpr int S(int p) { return p * LOGE; }
+    // Waves per SIMD the LDS footprint allows (160 KiB LDS, 2048 threads per
+    // CU): used as __launch_bounds__' min-waves-per-EU so the register
+    // allocation never costs a resident workgroup.
+    template <typename W>
+    static constexpr int occ_waves() {
+        const int by_lds = (160 * 1024) / (P * N * (int)sizeof(W));
+        const int by_thr = 2048 / THREADS;
+        const int wg = by_lds < by_thr ? by_lds : by_thr;
+        const int w = wg * THREADS / 64 / 4;
+#ifdef FHE_NO_OCC_BOUND
+        return 1;
+#else
+        return w < 1 ? 1 : (w > 8 ? 8 : w);
+#endif
+    }
     static constexpr int R(int p) { return (L - p * LOGE) < LOGE ? (L - p * LOGE) : LOGE; }
 };
 
@@ -129,82 +144,127 @@ __device__ __forceinline__ uint32_t gidx(uint32_t tau, int e) {
     return lay<S, R>(g_of<LOGN, PASS>(tau, u)) | (uint32_t(t) << S);
 }
 
-// ---------------------------------------------------------------- passes
-// Forward (CT) butterflies of pass PASS: stages S..S+R-1 ascending.
-template <int LOGN, int PASS, typename W>
-__device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], uint32_t tau, const Tw<W> *__restrict__ tw,
-                                         const Arith<W> &ar) {
+// ---------------------------------------------------------------- twiddles
+// Twiddles of one pass, loaded into VGPRs ahead of use: slot (k, u, tl) is
+// butterfly group tl of global stage S+k for slot-group u.  The loads of
+// pass p+1 are issued before the LDS exchange + barrier that precede it, so
+// their L2 latency overlaps the exchange.
+template <int LOGN, int PASS>
+struct PassTw {
     using G = Geo<LOGN>;
-    constexpr int S = G::S(PASS), R = G::R(PASS), NU = G::E >> R;
+    static constexpr int S = G::S(PASS), R = G::R(PASS), NU = G::E >> R;
+    static constexpr int PER_U = (1 << R) - 1;
+    static constexpr int COUNT = NU * PER_U;
+    static constexpr int slot(int k, int u, int tl) { return u * PER_U + ((1 << k) - 1) + tl; }
+};
+
+// PF = stages of a pass whose twiddles are loaded before the LDS exchange
+// (the rest right after it): trades VGPRs for hidden L2 latency.  Measured
+// on MI355X: 2 for the single-transform kernels (64-VGPR budget at two
+// workgroups per CU), 4 for polymul (one workgroup per CU).
+constexpr int kPfSingle = 2;
+constexpr int kPfPolymul = 4;
+
+template <int LOGN, int PASS, typename W, int K0 = 0, int K1 = 8>
+__device__ __forceinline__ void load_tw(uint32_t tau, const Tw<W> *__restrict__ tw,
+                                        Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT]) {
+    using P = PassTw<LOGN, PASS>;
+    constexpr int S = P::S, R = P::R, NU = P::NU;
+    constexpr int KE = K1 < R ? K1 : R;
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
+    for (int u = 0; u < NU; ++u) {
+        const uint32_t jlo = g_of<LOGN, PASS>(tau, u) & ((1u << S) - 1);
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const uint32_t jlo = g_of<LOGN, PASS>(tau, u) & ((1u << S) - 1);
+        for (int k = K0; k < KE; ++k)
 #pragma unroll
-            for (int t = 0; t < (1 << R); ++t) {
-                if (t & (1 << k)) continue;
-                const int e = t + (u << R), e2 = e + (1 << k);
-                const uint32_t j = jlo | (uint32_t(t & ((1 << k) - 1)) << S);
-                const Tw<W> w = tw[(1u << (S + k)) + j];
-                ar.ct(v[e], v[e2], w);
+            for (int tl = 0; tl < (1 << k); ++tl) {
+                const uint32_t idx = (1u << (S + k)) + (jlo | (uint32_t(tl) << S));
+                if constexpr (PASS == 0) {  // wave-uniform: scalar loads through the constant cache
+                    typedef const __attribute__((address_space(4))) W cw_t;
+                    const cw_t *cp = (const cw_t *)(const void *)tw;
+                    t[P::slot(k, u, tl)] = Tw<W>{cp[2 * idx], cp[2 * idx + 1]};
+                } else
+                    t[P::slot(k, u, tl)] = tw[idx];
             }
-        }
     }
+}
+
+// ---------------------------------------------------------------- passes
+// Forward (CT) butterflies of pass PASS: stages S..S+R-1 ascending.  LAZY:
+// no intermediate reduction (values grow by 2q per stage; valid when
+// (4 + 2L) q <= 2^W).
+template <int LOGN, int PASS, bool LAZY, typename W>
+__device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                         const Arith<W> &ar) {
+    using P = PassTw<LOGN, PASS>;
+    constexpr int R = P::R, NU = P::NU;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+            for (int tt = 0; tt < (1 << R); ++tt) {
+                if (tt & (1 << k)) continue;
+                const int e = tt + (u << R), e2 = e + (1 << k);
+                const Tw<W> w = t[P::slot(k, u, tt & ((1 << k) - 1))];
+                if constexpr (LAZY) ar.ct_lazy(v[e], v[e2], w);
+                else ar.ct(v[e], v[e2], w);
+            }
 }
 
 // Inverse (GS) butterflies of pass PASS: stages S+R-1..S descending.  When
 // FOLD, global stage 0 (w = 1) applies the N^-1 (or N^-1 * R) scaling.
 template <int LOGN, int PASS, bool FOLD, typename W>
-__device__ __forceinline__ void inv_pass(W (&v)[Geo<LOGN>::E], uint32_t tau, const Tw<W> *__restrict__ tw,
+__device__ __forceinline__ void inv_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
                                          const Arith<W> &ar, Tw<W> scale) {
-    using G = Geo<LOGN>;
-    constexpr int S = G::S(PASS), R = G::R(PASS), NU = G::E >> R;
+    using P = PassTw<LOGN, PASS>;
+    constexpr int S = P::S, R = P::R, NU = P::NU;
 #pragma unroll
-    for (int k = R - 1; k >= 0; --k) {
+    for (int k = R - 1; k >= 0; --k)
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const uint32_t jlo = g_of<LOGN, PASS>(tau, u) & ((1u << S) - 1);
+        for (int u = 0; u < NU; ++u)
 #pragma unroll
-            for (int t = 0; t < (1 << R); ++t) {
-                if (t & (1 << k)) continue;
-                const int e = t + (u << R), e2 = e + (1 << k);
-                if (FOLD && S + k == 0) {
-                    ar.gs_scaled(v[e], v[e2], scale);
-                } else {
-                    const uint32_t j = jlo | (uint32_t(t & ((1 << k) - 1)) << S);
-                    const Tw<W> w = tw[(1u << (S + k)) + j];
-                    ar.gs(v[e], v[e2], w);
-                }
+            for (int tt = 0; tt < (1 << R); ++tt) {
+                if (tt & (1 << k)) continue;
+                const int e = tt + (u << R), e2 = e + (1 << k);
+                if (FOLD && S + k == 0) ar.gs_scaled(v[e], v[e2], scale);
+                else ar.gs(v[e], v[e2], t[P::slot(k, u, tt & ((1 << k) - 1))]);
             }
-        }
-    }
 }
 
-// Passes 1..NP-1 of the forward transform, exchanging through LDS.
-template <int LOGN, int PASS, typename W>
+// Passes PASS..NP-1 of the forward transform, exchanging through LDS.
+template <int LOGN, int PASS, bool LAZY, int PF, typename W>
 __device__ __forceinline__ void fwd_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const Tw<W> *__restrict__ tw,
                                          const Arith<W> &ar) {
     using G = Geo<LOGN>;
     if constexpr (PASS < G::NP) {
+        Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);  // in flight across the exchange
         lds_store<LOGN, PASS - 1>(lds, v, tau);
         __syncthreads();
         lds_load<LOGN, PASS>(lds, v, tau);
-        fwd_pass<LOGN, PASS>(v, tau, tw, ar);
-        fwd_rest<LOGN, PASS + 1>(lds, v, tau, tw, ar);
+        load_tw<LOGN, PASS, W, PF, 8>(tau, tw, t);
+        fwd_pass<LOGN, PASS, LAZY>(v, t, ar);
+        fwd_rest<LOGN, PASS + 1, LAZY, PF>(lds, v, tau, tw, ar);
     }
 }
 
 // Passes PASS..0 of the inverse transform (PASS+1 already in registers).
-template <int LOGN, int PASS, bool FOLD, typename W>
+template <int LOGN, int PASS, bool FOLD, int PF, typename W>
 __device__ __forceinline__ void inv_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const Tw<W> *__restrict__ tw,
                                          const Arith<W> &ar, Tw<W> scale) {
     if constexpr (PASS >= 0) {
+        Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        // inverse stages run k = R-1 .. 0: prefetch the top ones
+        constexpr int R = PassTw<LOGN, PASS>::R;
+        constexpr int KS = R - PF < 0 ? 0 : R - PF;
+        load_tw<LOGN, PASS, W, KS, 8>(tau, tw, t);
         lds_store<LOGN, PASS + 1>(lds, v, tau);
         __syncthreads();
         lds_load<LOGN, PASS>(lds, v, tau);
-        inv_pass<LOGN, PASS, FOLD>(v, tau, tw, ar, scale);
-        inv_rest<LOGN, PASS - 1, FOLD>(lds, v, tau, tw, ar, scale);
+        load_tw<LOGN, PASS, W, 0, KS>(tau, tw, t);
+        inv_pass<LOGN, PASS, FOLD>(v, t, ar, scale);
+        inv_rest<LOGN, PASS - 1, FOLD, PF>(lds, v, tau, tw, ar, scale);
     }
 }
 
@@ -221,38 +281,78 @@ struct NttArgs {
     Tw<W> ninv;            // N^-1
     Tw<W> ninv_r;          // N^-1 * R  (after a Montgomery pointwise product)
     Tw<W> rmod;            // R mod q  (to Montgomery form)
+    Tw<W> one;             // {1, floor(2^W / q)}: shoup(x, one) = x mod q in [0, 2q)
 };
+
+// Any forward-transform output (< (4+2L) q when LAZY, < 4q otherwise) to
+// [0, 2q) / to canonical.
+template <bool LAZY, typename W>
+__device__ __forceinline__ W fwd_to_2q(W x, const NttArgs<W> &A) {
+    if constexpr (LAZY) return A.ar.shoup(x, A.one);
+    else return A.ar.red2q(x);
+}
+template <bool LAZY, typename W>
+__device__ __forceinline__ W fwd_to_canon(W x, const NttArgs<W> &A) {
+    return A.ar.red1q(fwd_to_2q<LAZY>(x, A));
+}
+
+// E coefficients of one polynomial from HBM into the lazy range [0, lim) of
+// word W.  Out-of-range inputs (any u64 behaves as x mod q) take one
+// divergent slow path for the whole thread.
+template <int E, typename W, typename F>
+__device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q, uint64_t mu, F &&addr_of) {
+    uint64_t raw[E];
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < E; ++t) {
+        raw[t] = addr_of(t);
+        bad |= raw[t] >= lim;
+    }
+    if (__builtin_expect(bad, 0)) {
+#pragma unroll
+        for (int t = 0; t < E; ++t)
+            if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+    }
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
+}
 
 // Forward transform of one polynomial held by this thread group: HBM load
 // (bit-reversed, coalesced), all passes; result left in v (last layout,
-// values in [0, 4q)).
-template <int LOGN, bool NEGA, typename W>
+// values in [0, 4q), or [0, (4+2L)q) when LAZY).
+template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, typename W>
 __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const uint64_t *__restrict__ src,
                                          bool valid, const NttArgs<W> &A) {
     using G = Geo<LOGN>;
+    Tw<W> t0[PassTw<LOGN, 0>::COUNT];
+    load_tw<LOGN, 0>(tau, A.twf, t0);
     const uint64_t lim = NEGA ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
+    load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+        return valid ? __builtin_nontemporal_load(src + tau + cbrv(t, G::LOGE) * G::T) : 0;
+    });
+    if constexpr (NEGA) {
 #pragma unroll
-    for (int t = 0; t < G::E; ++t) {
-        const uint32_t gi = tau + cbrv(t, G::LOGE) * G::T;
-        uint64_t x = valid ? __builtin_nontemporal_load(src + gi) : 0;
-        v[t] = load_lazy<W>(x, lim, A.q64, A.mu64);
-        if constexpr (NEGA) v[t] = A.ar.shoup(v[t], A.twist[gi]);
+        for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tau + cbrv(t, G::LOGE) * G::T]);
     }
-    fwd_pass<LOGN, 0>(v, tau, A.twf, A.ar);
-    fwd_rest<LOGN, 1>(lds, v, tau, A.twf, A.ar);
+    fwd_pass<LOGN, 0, LAZY>(v, t0, A.ar);
+    fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar);
 }
 
 // Inverse transform from v (last-pass layout, values in [0, 2q)) to HBM
 // (bit-reversed store, coalesced), canonical output.  scale = N^-1 or
 // N^-1 * R; post = the matching negacyclic post-twist table.
-template <int LOGN, bool NEGA, typename W>
+template <int LOGN, bool NEGA, int PF = kPfSingle, typename W>
 __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, uint64_t *__restrict__ dst,
                                                    bool valid, const NttArgs<W> &A, Tw<W> scale,
                                                    const Tw<W> *__restrict__ post) {
     using G = Geo<LOGN>;
     constexpr int LAST = G::NP - 1;
-    inv_pass<LOGN, LAST, !NEGA>(v, tau, A.twi, A.ar, scale);
-    inv_rest<LOGN, LAST - 1, !NEGA>(lds, v, tau, A.twi, A.ar, scale);
+    {
+        Tw<W> t[PassTw<LOGN, LAST>::COUNT];
+        load_tw<LOGN, LAST>(tau, A.twi, t);
+        inv_pass<LOGN, LAST, !NEGA>(v, t, A.ar, scale);
+    }
+    inv_rest<LOGN, LAST - 1, !NEGA, PF>(lds, v, tau, A.twi, A.ar, scale);
 #pragma unroll
     for (int t = 0; t < G::E; ++t) {
         const uint32_t gi = tau + cbrv(t, G::LOGE) * G::T;
@@ -262,4 +362,4 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
     }
 }
 
-}  // namespace fhe
+}  // namespace FHE_NS

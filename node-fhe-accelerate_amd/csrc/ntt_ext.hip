@@ -16,10 +16,10 @@
 // end -- (k+1)L + (k+1) transforms, one kernel, one HBM pass over the GLWE.
 #include "fhe_internal.hpp"
 
-namespace fhe {
+namespace FHE_NS {
 
-template <int LOGN, typename W, bool NEGA, int K1>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+template <int LOGN, typename W, bool NEGA, int K1, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, uint64_t *__restrict__ out,
           size_t batch, int level, int base_log, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -43,25 +43,28 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
         const uint64_t *src = glwe + (poly * K1 + i) * G::N;
         if (r > 0 && G::NP > 1) __syncthreads();
         W v[G::E];
-#pragma unroll
-        for (int t = 0; t < G::E; ++t) {
-            const uint32_t gi = tau + cbrv(t, G::LOGE) * G::T;
-            const uint64_t c = valid ? src[gi] : 0;
+        Tw<W> t0[PassTw<LOGN, 0>::COUNT];
+        load_tw<LOGN, 0>(tau, A.twf, t0);
+        load_coeffs<G::E>(v, lim, q, A.mu64, [&](int t) -> uint64_t {
+            const uint64_t c = valid ? src[tau + cbrv(t, G::LOGE) * G::T] : 0;
             uint64_t d = (c >> shift) & mask;
             if (d > half) {
                 d = q - (base - d);
                 if (d >= q) d = mod64_slow(d, q, A.mu64);
             }
-            v[t] = load_lazy<W>(d, lim, q, A.mu64);
-            if constexpr (NEGA) v[t] = A.ar.shoup(v[t], A.twist[gi]);
+            return d;
+        });
+        if constexpr (NEGA) {
+#pragma unroll
+            for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tau + cbrv(t, G::LOGE) * G::T]);
         }
-        fwd_pass<LOGN, 0>(v, tau, A.twf, A.ar);
-        fwd_rest<LOGN, 1>(lds, v, tau, A.twf, A.ar);
+        fwd_pass<LOGN, 0, LAZY>(v, t0, A.ar);
+        fwd_rest<LOGN, 1, LAZY, kPfSingle>(lds, v, tau, A.twf, A.ar);
         const uint64_t *g = ggsw + (size_t)r * K1 * G::N;
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
-            const W d = A.ar.red2q(v[e]);
+            const W d = fwd_to_2q<LAZY>(v[e], A);
 #pragma unroll
             for (int j = 0; j < K1; ++j)
                 acc[j][e] = A.ar.red2q(acc[j][e] + A.ar.mont(d, (W)g[(size_t)j * G::N + gi]));
@@ -80,8 +83,8 @@ static hipError_t ext_one(const NttArgs<W> &A, hipStream_t s, int k1, int level,
     using G = Geo<LOGN>;
     const size_t blocks = (batch + G::P - 1) / G::P;
     if (k1 != 2) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_extprod<LOGN, W, NEGA, 2>), dim3(blocks), dim3(G::THREADS), 0, s, glwe, ggsw, out, batch,
-                       level, base_log, A);
+    hipLaunchKernelGGL((k_extprod<LOGN, W, NEGA, 2, false>), dim3(blocks), dim3(G::THREADS), 0, s, glwe, ggsw, out,
+                       batch, level, base_log, A);
     return hipGetLastError();
 }
 
@@ -108,4 +111,4 @@ hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const 
                   : ext_dispatch<uint64_t, false>(p, p.a64, k1, level, base_log, glwe, ggsw, out, batch);
 }
 
-}  // namespace fhe
+}  // namespace FHE_NS

@@ -4,10 +4,10 @@
 // polynomial_ring.cpp:104-116, 493-530).
 #include "fhe_internal.hpp"
 
-namespace fhe {
+namespace FHE_NS {
 
-template <int LOGN, typename W, bool NEGA, int EPI>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+template <int LOGN, typename W, bool NEGA, bool LAZY, int EPI>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::N];
@@ -16,20 +16,20 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::N;
     W v[G::E];
-    fwd_poly<LOGN, NEGA>(lds, v, tau, in + poly * G::N, valid, A);
+    fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     uint64_t *dst = out + poly * G::N;
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         W x = v[e];
         if constexpr (EPI == 1) x = A.ar.red1q(A.ar.shoup(x, A.rmod));
-        else x = A.ar.canon4(x);
+        else x = fwd_to_canon<LAZY>(x, A);
         __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, e));
     }
 }
 
-template <int LOGN, typename W, bool NEGA>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+template <int LOGN, typename W, bool NEGA, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
               size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -39,7 +39,7 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::N;
     W v[G::E];
-    fwd_poly<LOGN, NEGA>(lds, v, tau, in + poly * G::N, valid, A);
+    fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     const uint64_t *wp = wv + poly * G::N;
     uint64_t *dst = out + poly * G::N;
@@ -49,23 +49,31 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
         // w * R mod q (Montgomery form) in [0, 2q); exact for any u64 w.
         W wm = A.ar.mont(load_lazy<W>(__builtin_nontemporal_load(wp + gi), wlim, A.q64, A.mu64), A.ar.r2);
-        W x = A.ar.red1q(A.ar.mont(A.ar.red2q(v[e]), wm));
+        W x = A.ar.red1q(A.ar.mont(fwd_to_2q<LAZY>(v[e], A), wm));
         __builtin_nontemporal_store((uint64_t)x, dst + gi);
     }
 }
 
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W, bool NEGA, bool LAZY>
 static hipError_t fwd_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *in, uint64_t *out, size_t batch,
                           int epi, const uint64_t *wv) {
     using G = Geo<LOGN>;
     const size_t blocks = (batch + G::P - 1) / G::P;
     if (wv)
-        hipLaunchKernelGGL((k_ntt_fwd_mul<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, in, wv, out, batch, A);
+        hipLaunchKernelGGL((k_ntt_fwd_mul<LOGN, W, NEGA, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, in, wv, out,
+                           batch, A);
     else if (epi == 1)
-        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, 1>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, LAZY, 1>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
     else
-        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, 0>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, LAZY, 0>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
     return hipGetLastError();
+}
+template <int LOGN, typename W, bool NEGA>
+static hipError_t fwd_lazy(const Plan &p, const NttArgs<W> &A, const uint64_t *in, uint64_t *out, size_t batch,
+                           int epi, const uint64_t *wv) {
+    if constexpr (sizeof(W) == 4)
+        if (p.lazy) return fwd_one<LOGN, W, NEGA, true>(A, p.stream, in, out, batch, epi, wv);
+    return fwd_one<LOGN, W, NEGA, false>(A, p.stream, in, out, batch, epi, wv);
 }
 
 template <typename W, bool NEGA>
@@ -73,7 +81,7 @@ static hipError_t fwd_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_
                                int epi, const uint64_t *wv) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return fwd_one<L, W, NEGA>(A, p.stream, in, out, batch, epi, wv);
+    case L: return fwd_lazy<L, W, NEGA>(p, A, in, out, batch, epi, wv);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -98,4 +106,4 @@ hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, u
     return fwd_any(p, a, out, batch, 0, w);
 }
 
-}  // namespace fhe
+}  // namespace FHE_NS

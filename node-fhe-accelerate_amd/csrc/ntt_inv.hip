@@ -6,10 +6,10 @@
 // inverse's N^-1 scaling).
 #include "fhe_internal.hpp"
 
-namespace fhe {
+namespace FHE_NS {
 
 template <int LOGN, typename W, bool NEGA>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::N];
@@ -28,7 +28,9 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     inv_poly_from_regs<LOGN, NEGA>(lds, v, tau, out + poly * G::N, valid, A, A.ninv, A.untwist);
 }
 
-template <int LOGN, typename W, bool NEGA>
+// Two spectra in flight: no occupancy bound (the LDS-permitted second
+// workgroup would cost spills).
+template <int LOGN, typename W, bool NEGA, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS)
 k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *__restrict__ c, size_t batch,
           NttArgs<W> A) {
@@ -39,22 +41,29 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::N;
     W va[G::E], vb[G::E];
-    fwd_poly<LOGN, NEGA>(lds, va, tau, a + poly * G::N, valid, A);
-    if constexpr (G::NP > 1) __syncthreads();  // LDS is reused by the second transform
-    fwd_poly<LOGN, NEGA>(lds, vb, tau, b + poly * G::N, valid, A);
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, va, tau, a + poly * G::N, valid, A);
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) vb[e] = A.ar.mont(A.ar.red2q(va[e]), A.ar.red2q(vb[e]));  // a*b*R^-1
+    for (int e = 0; e < G::E; ++e) va[e] = fwd_to_2q<LAZY>(va[e], A);
+    if constexpr (G::NP > 1) __syncthreads();  // LDS is reused by the second transform
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, vb, tau, b + poly * G::N, valid, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) vb[e] = A.ar.mont(va[e], fwd_to_2q<LAZY>(vb[e], A));  // a*b*R^-1
     if constexpr (G::NP > 1) __syncthreads();
-    inv_poly_from_regs<LOGN, NEGA>(lds, vb, tau, c + poly * G::N, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, vb, tau, c + poly * G::N, valid, A, A.ninv_r, A.untwist_r);
 }
 
 template <int LOGN, typename W, bool NEGA>
-static hipError_t inv_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *a, const uint64_t *b, uint64_t *c,
-                          size_t batch) {
+static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, const uint64_t *a, const uint64_t *b,
+                          uint64_t *c, size_t batch) {
     using G = Geo<LOGN>;
     const size_t blocks = (batch + G::P - 1) / G::P;
-    if (b)
-        hipLaunchKernelGGL((k_polymul<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, b, c, batch, A);
+    bool lazy = false;
+    if constexpr (sizeof(W) == 4) lazy = p.lazy;
+    if (b && lazy) {
+        if constexpr (sizeof(W) == 4)
+            hipLaunchKernelGGL((k_polymul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, s, a, b, c, batch, A);
+    } else if (b)
+        hipLaunchKernelGGL((k_polymul<LOGN, W, NEGA, false>), dim3(blocks), dim3(G::THREADS), 0, s, a, b, c, batch, A);
     else
         hipLaunchKernelGGL((k_ntt_inv<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, c, batch, A);
     return hipGetLastError();
@@ -65,7 +74,7 @@ static hipError_t inv_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_
                                uint64_t *c, size_t batch) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return inv_one<L, W, NEGA>(A, p.stream, a, b, c, batch);
+    case L: return inv_one<L, W, NEGA>(p, A, p.stream, a, b, c, batch);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -89,4 +98,4 @@ hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, u
     return inv_any(p, a, b, c, batch);
 }
 
-}  // namespace fhe
+}  // namespace FHE_NS

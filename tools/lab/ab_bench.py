@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Kernel timing of ONE libfhe_gpu variant (lab tool; tools/gpu_ab.sh
+interleaves variants across processes and rounds).
+
+usage: FHE_GPU_LIB=build/libfhe_gpu_x.so ab_bench.py TAG [--ops fwd_mul,polymul] [--qs ...]
+Prints one line per (op, q): TAG op q kernel_ms checksum.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "node-fhe-accelerate_amd"))
+import torch  # noqa: E402
+import fhe_gpu  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("tag")
+ap.add_argument("--ops", default="fwd_mul,polymul")
+ap.add_argument("--qs", default="132120577,4611686018326724609")
+ap.add_argument("--n", type=int, default=16384)
+ap.add_argument("--batch", type=int, default=65536)
+ap.add_argument("--steps", type=int, default=5)
+args = ap.parse_args()
+n, B = args.n, args.batch
+for q in [int(x) for x in args.qs.split(",")]:
+    g = torch.Generator(device="cuda").manual_seed(7)
+    a = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
+    b = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
+    out = torch.empty_like(a)
+    ring = fhe_gpu.PolynomialRing(n, q)
+    for op in args.ops.split(","):
+        fn = {"fwd_mul": lambda: ring.forward_ntt_mul(a, b, out=out),
+              "polymul": lambda: ring.multiply(a, b, out=out),
+              "fwd": lambda: ring.forward_ntt(a, out=out),
+              "inv": lambda: ring.inverse_ntt(a, out=out)}[op]
+        fn()
+        torch.cuda.synchronize()
+        chk = int(out[:8].sum().item()) ^ int(out[-8:].sum().item())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.steps
+        print(f"AB {args.tag} {op} {q} {ms:.4f} {chk}", flush=True)
+    del a, b, out
+    torch.cuda.empty_cache()
