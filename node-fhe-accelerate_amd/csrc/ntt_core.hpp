@@ -16,13 +16,32 @@
 //     the store of the last inverse pass: every HBM access is coalesced;
 //   * twiddles come from a stage-major table tw[2^s + j] (L2 resident);
 //     pass-0 twiddles are wave-uniform (scalar loads);
-//   * LDS addresses are XOR-swizzled per degree so every ds_read/ds_write
-//     of the pass layouts is bank-conflict free (masks found by exhaustive
-//     simulation of the access patterns).
+//   * LDS uses a padded layout (pad_idx) so every access of a pass is one
+//     base + an immediate offset, with few bank conflicts.
 #pragma once
 #include "fhe_arith.hpp"
 
 namespace FHE_NS {
+
+// Padded LDS layout: element i lives at word i + (i >> A) + (i >> B)
+// (A, B per degree; 0 = unused).  For every pass layout the padded address
+// of (g, t) splits as pad(lay(g)) + pad(t << S), so each thread computes one
+// base per slot group and every ds_read/ds_write of the pass uses an
+// immediate offset.  Pads chosen by simulating the lane groups of every pass
+// layout: conflict-free up to N = 256, one 2-way
+// conflicted exchange above.  An XOR swizzle (conflict-free everywhere) was
+// replaced because its 16 per-layout addresses stayed live across whole
+// kernels (64 VGPRs in polymul, forcing scratch spills).
+constexpr int kPadA[17] = {0, 0, 0, 0, 0, 3, 3, 3, 4, 5, 5, 6, 7, 8, 5, 5, 0};
+constexpr int kPadB[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 10, 10, 0};
+
+template <int L>
+__host__ __device__ constexpr uint32_t pad_idx(uint32_t i) {
+    return i + (kPadA[L] ? (i >> kPadA[L]) : 0u) + (kPadB[L] ? (i >> kPadB[L]) : 0u);
+}
+// LDS words per polynomial
+template <int L>
+constexpr int lds_words() { return (int)pad_idx<L>((1u << L) - 1) + 1; }
 
 // ---------------------------------------------------------------- geometry
 template <int LOGN>
@@ -36,13 +55,14 @@ struct Geo {
     static constexpr int NP = (L + LOGE - 1) / LOGE;  // passes
     static constexpr int P = T >= 256 ? 1 : 256 / T;  // polynomials per workgroup
     static constexpr int THREADS = T * P;
+    static constexpr int LW = lds_words<L>();  // padded LDS words per polynomial
     static constexpr int S(int p) { return p * LOGE; }
     // Waves per SIMD the LDS footprint allows (160 KiB LDS, 2048 threads per
     // CU): used as __launch_bounds__' min-waves-per-EU so the register
     // allocation never costs a resident workgroup.
     template <typename W>
     static constexpr int occ_waves() {
-        const int by_lds = (160 * 1024) / (P * N * (int)sizeof(W));
+        const int by_lds = (160 * 1024) / (P * LW * (int)sizeof(W));
         const int by_thr = 2048 / THREADS;
         const int wg = by_lds < by_thr ? by_lds : by_thr;
         const int w = wg * THREADS / 64 / 4;
@@ -59,38 +79,6 @@ __host__ __device__ constexpr uint32_t cbrv(uint32_t x, int bits) {
     uint32_t r = 0;
     for (int i = 0; i < bits; ++i) { r = (r << 1) | (x & 1); x >>= 1; }
     return r;
-}
-
-// XOR swizzle masks: bit b (b >= 5) of a coefficient index flips these low
-// bits.  kSwz[L][b].  Zero-conflict for L >= 9 under the pass layouts.
-constexpr uint32_t kSwz[17][17] = {
-    {}, {}, {}, {}, {}, {},
-    /* 6 */ {0, 0, 0, 0, 0, 11},
-    /* 7 */ {0, 0, 0, 0, 0, 3, 6},
-    /* 8 */ {0, 0, 0, 0, 0, 24, 2, 28},
-    /* 9 */ {0, 0, 0, 0, 0, 7, 1, 28, 21},
-    /*10 */ {0, 0, 0, 0, 0, 2, 27, 30, 31, 13},
-    /*11 */ {0, 0, 0, 0, 0, 2, 15, 9, 20, 1, 30},
-    /*12 */ {0, 0, 0, 0, 0, 30, 17, 22, 17, 24, 29, 23},
-    /*13 */ {0, 0, 0, 0, 0, 17, 22, 4, 31, 10, 14, 23, 28},
-    /*14 */ {0, 0, 0, 0, 0, 10, 17, 24, 31, 18, 11, 26, 29, 5},
-    /*15 */ {0, 0, 0, 0, 0, 13, 21, 2, 19, 22, 1, 3, 9, 23, 15},
-    {},
-};
-
-template <int L>
-__host__ __device__ constexpr uint32_t swz_c(uint32_t i) {
-    uint32_t a = i;
-    for (int b = 5; b < L; ++b)
-        if ((i >> b) & 1) a ^= kSwz[L][b];
-    return a;
-}
-template <int L>
-__device__ __forceinline__ uint32_t swz_rt(uint32_t i) {
-    uint32_t a = i;
-#pragma unroll
-    for (int b = 5; b < L; ++b) a ^= ((i >> b) & 1) ? kSwz[L][b] : 0u;
-    return a;
 }
 
 // Position of element (g, t) in pass layout (S, R): t occupies bits
@@ -116,10 +104,9 @@ __device__ __forceinline__ void lds_store(W *lds, const W (&v)[Geo<LOGN>::E], ui
     constexpr int S = G::S(PASS), R = G::R(PASS), NU = G::E >> R;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-        uint32_t base = swz_rt<LOGN>(lay<S, R>(g_of<LOGN, PASS>(tau, u)));
+        const uint32_t base = pad_idx<LOGN>(lay<S, R>(g_of<LOGN, PASS>(tau, u)));
 #pragma unroll
-        for (int t = 0; t < (1 << R); ++t)
-            lds[base ^ swz_c<LOGN>(uint32_t(t) << S)] = v[t + (u << R)];
+        for (int t = 0; t < (1 << R); ++t) lds[base + pad_idx<LOGN>(uint32_t(t) << S)] = v[t + (u << R)];
     }
 }
 template <int LOGN, int PASS, typename W>
@@ -128,10 +115,9 @@ __device__ __forceinline__ void lds_load(const W *lds, W (&v)[Geo<LOGN>::E], uin
     constexpr int S = G::S(PASS), R = G::R(PASS), NU = G::E >> R;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-        uint32_t base = swz_rt<LOGN>(lay<S, R>(g_of<LOGN, PASS>(tau, u)));
+        const uint32_t base = pad_idx<LOGN>(lay<S, R>(g_of<LOGN, PASS>(tau, u)));
 #pragma unroll
-        for (int t = 0; t < (1 << R); ++t)
-            v[t + (u << R)] = lds[base ^ swz_c<LOGN>(uint32_t(t) << S)];
+        for (int t = 0; t < (1 << R); ++t) v[t + (u << R)] = lds[base + pad_idx<LOGN>(uint32_t(t) << S)];
     }
 }
 // Global (natural-order) index of slot e in pass layout PASS (PASS > 0, or

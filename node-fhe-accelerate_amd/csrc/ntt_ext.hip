@@ -23,11 +23,11 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_wa
 k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, uint64_t *__restrict__ out,
           size_t batch, int level, int base_log, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::N];
+    __shared__ W lds_all[G::P * G::LW];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::N;
+    W *lds = lds_all + pl * G::LW;
     W acc[K1][G::E];
 #pragma unroll
     for (int j = 0; j < K1; ++j)

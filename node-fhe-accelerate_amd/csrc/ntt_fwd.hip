@@ -10,11 +10,11 @@ template <int LOGN, typename W, bool NEGA, bool LAZY, int EPI>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::N];
+    __shared__ W lds_all[G::P * G::LW];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::N;
+    W *lds = lds_all + pl * G::LW;
     W v[G::E];
     fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
@@ -33,11 +33,11 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_wa
 k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
               size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::N];
+    __shared__ W lds_all[G::P * G::LW];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::N;
+    W *lds = lds_all + pl * G::LW;
     W v[G::E];
     fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;

@@ -12,11 +12,11 @@ template <int LOGN, typename W, bool NEGA>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::N];
+    __shared__ W lds_all[G::P * G::LW];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::N;
+    W *lds = lds_all + pl * G::LW;
     W v[G::E];
     const uint64_t *src = in + poly * G::N;
     const uint64_t lim = (uint64_t)A.ar.q2;  // GS inputs must be < 2q
@@ -28,28 +28,55 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     inv_poly_from_regs<LOGN, NEGA>(lds, v, tau, out + poly * G::N, valid, A, A.ninv, A.untwist);
 }
 
-// Two spectra in flight: no occupancy bound (the LDS-permitted second
-// workgroup would cost spills).
+// Where fwd(a) waits while fwd(b) runs: 0 = VGPRs (small N), 1 = a second
+// LDS region, 2 = the output row in HBM (u64 at N = 16384, where LDS is
+// full and the kernel is ALU-bound, so 16N extra bytes are cheap).  Keeping
+// both spectra in VGPRs cost 150-255 VGPRs (N <= 8192) or scratch spills
+// (N = 16384).
+template <int LOGN, typename W>
+constexpr int polymul_stash() {
+    using G = Geo<LOGN>;
+    if (LOGN < 5) return 0;
+    return G::P * (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024 ? 1 : 2;
+}
+
 template <int LOGN, typename W, bool NEGA, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS)
-k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *__restrict__ c, size_t batch,
+k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
           NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::N];
+    constexpr int STASH = polymul_stash<LOGN, W>();
+    __shared__ W lds_all[G::P * G::LW + (STASH == 1 ? G::P * G::N : 0)];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::N;
-    W va[G::E], vb[G::E];
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, va, tau, a + poly * G::N, valid, A);
+    W *lds = lds_all + pl * G::LW;
+    W *st = lds_all + G::P * G::LW + pl * G::N;
+    uint64_t *crow = c + poly * G::N;
+    W v[G::E];
+    W va[STASH == 0 ? G::E : 1];
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, a + poly * G::N, valid, A);
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) va[e] = fwd_to_2q<LAZY>(va[e], A);
-    if constexpr (G::NP > 1) __syncthreads();  // LDS is reused by the second transform
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, vb, tau, b + poly * G::N, valid, A);
+    for (int e = 0; e < G::E; ++e) {
+        const W x = fwd_to_2q<LAZY>(v[e], A);
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);  // own positions: no sync needed
+        if constexpr (STASH == 0) va[e] = x;
+        else if constexpr (STASH == 1) st[gi] = x;
+        else if (valid) crow[gi] = (uint64_t)x;
+    }
+    if constexpr (G::NP > 1) __syncthreads();  // LDS exchange buffer is reused by the second transform
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, b + poly * G::N, valid, A);
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) vb[e] = A.ar.mont(va[e], fwd_to_2q<LAZY>(vb[e], A));  // a*b*R^-1
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
+        W x;
+        if constexpr (STASH == 0) x = va[e];
+        else if constexpr (STASH == 1) x = st[gi];
+        else x = valid ? (W)crow[gi] : W(0);
+        v[e] = A.ar.mont(x, fwd_to_2q<LAZY>(v[e], A));  // a*b*R^-1 in [0, 2q)
+    }
     if constexpr (G::NP > 1) __syncthreads();
-    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, vb, tau, c + poly * G::N, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tau, crow, valid, A, A.ninv_r, A.untwist_r);
 }
 
 template <int LOGN, typename W, bool NEGA>
@@ -95,6 +122,9 @@ hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t b
     return inv_any(p, in, nullptr, out, batch);
 }
 hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch) {
+    // The HBM stash writes fwd(a) into c before b is read: if c aliases b,
+    // transform b first (the pointwise product commutes).
+    if (c == b) { const uint64_t *t = a; a = b; b = t; }
     return inv_any(p, a, b, c, batch);
 }
 
