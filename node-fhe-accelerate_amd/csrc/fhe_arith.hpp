@@ -38,7 +38,15 @@ struct Arith {
     // x in [0, 2^W): x*w mod q, lazy result in [0, 2q)   (Shoup)
     __device__ __forceinline__ W shoup(W x, W w, W wp) const {
         W h = mulhi(x, wp);
-        return x * w - h * q;
+#ifndef FHE_SHOUP_MAD
+#define FHE_SHOUP_MAD 1
+#endif
+        if constexpr (sizeof(W) == 4 && FHE_SHOUP_MAD) {
+            // x*w - h*q (mod 2^32) as one v_mad_u64_u32: h*(2^32 - q) + x*w
+            return (W)((uint64_t)h * (uint32_t)(0u - q) + (uint32_t)(x * w));
+        } else {
+            return x * w - h * q;
+        }
     }
     __device__ __forceinline__ W shoup(W x, Tw<W> t) const { return shoup(x, t.w, t.wp); }
 
@@ -65,6 +73,15 @@ struct Arith {
     __device__ __forceinline__ void ct_lazy(W &x, W &y, Tw<W> t) const {
         W b = shoup(y, t);
         W a = x;
+        x = a + b;
+        y = a - b + q2;
+    }
+    // Stage-0 butterfly that also multiplies by R = 2^W (twiddle 1 -> R):
+    // puts the transform in Montgomery form for a following pointwise
+    // Montgomery product.  Outputs in [0, 4q) for any inputs < 2^W.
+    __device__ __forceinline__ void ct_rscale(W &x, W &y, Tw<W> r) const {
+        W a = shoup(x, r);
+        W b = shoup(y, r);
         x = a + b;
         y = a - b + q2;
     }

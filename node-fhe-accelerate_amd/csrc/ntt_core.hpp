@@ -179,9 +179,10 @@ __device__ __forceinline__ void load_tw(uint32_t tau, const Tw<W> *__restrict__ 
 // Forward (CT) butterflies of pass PASS: stages S..S+R-1 ascending.  LAZY:
 // no intermediate reduction (values grow by 2q per stage; valid when
 // (4 + 2L) q <= 2^W).
-template <int LOGN, int PASS, bool LAZY, typename W>
+// RS (pass 0 only): global stage 0 multiplies by R (ct_rscale).
+template <int LOGN, int PASS, bool LAZY, typename W, bool RS = false>
 __device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                         const Arith<W> &ar) {
+                                         const Arith<W> &ar, Tw<W> rmod = Tw<W>{}) {
     using P = PassTw<LOGN, PASS>;
     constexpr int R = P::R, NU = P::NU;
 #pragma unroll
@@ -193,7 +194,8 @@ __device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[
                 if (tt & (1 << k)) continue;
                 const int e = tt + (u << R), e2 = e + (1 << k);
                 const Tw<W> w = t[P::slot(k, u, tt & ((1 << k) - 1))];
-                if constexpr (LAZY) ar.ct_lazy(v[e], v[e2], w);
+                if (RS && PASS == 0 && k == 0) ar.ct_rscale(v[e], v[e2], rmod);
+                else if constexpr (LAZY) ar.ct_lazy(v[e], v[e2], w);
                 else ar.ct(v[e], v[e2], w);
             }
 }
@@ -305,14 +307,17 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
 
 // Forward transform of one polynomial held by this thread group: HBM load
 // (bit-reversed, coalesced), all passes; result left in v (last layout,
-// values in [0, 4q), or [0, (4+2L)q) when LAZY).
-template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, typename W>
+// values in [0, 4q), or [0, (4+2L)q) when LAZY; every bound is <= R, so a
+// raw output times a canonical residue is a valid Montgomery operand pair).
+// RS: the result is the transform times R (Montgomery form).
+template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, bool RS = false, typename W>
 __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const uint64_t *__restrict__ src,
                                          bool valid, const NttArgs<W> &A) {
     using G = Geo<LOGN>;
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
     load_tw<LOGN, 0>(tau, A.twf, t0);
-    const uint64_t lim = NEGA ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
+    // Shoup-based first steps (twist / R-scaling) accept any word
+    const uint64_t lim = (NEGA || RS) ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
         return valid ? __builtin_nontemporal_load(src + tau + cbrv(t, G::LOGE) * G::T) : 0;
     });
@@ -320,7 +325,7 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
 #pragma unroll
         for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tau + cbrv(t, G::LOGE) * G::T]);
     }
-    fwd_pass<LOGN, 0, LAZY>(v, t0, A.ar);
+    fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
     fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar);
 }
 

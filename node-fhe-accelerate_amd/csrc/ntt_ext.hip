@@ -64,7 +64,7 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
             const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
-            const W d = fwd_to_2q<LAZY>(v[e], A);
+            const W d = v[e];  // raw output (< R) times a canonical key: valid Montgomery pair
 #pragma unroll
             for (int j = 0; j < K1; ++j)
                 acc[j][e] = A.ar.red2q(acc[j][e] + A.ar.mont(d, (W)g[(size_t)j * G::N + gi]));

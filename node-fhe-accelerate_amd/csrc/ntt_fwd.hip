@@ -16,14 +16,13 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
     W v[G::E];
-    fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, in + poly * G::N, valid, A);
+    // EPI 1: transform times R (Montgomery form), folded into stage 0
+    fwd_poly<LOGN, NEGA, LAZY, kPfSingle, EPI == 1>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     uint64_t *dst = out + poly * G::N;
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
-        W x = v[e];
-        if constexpr (EPI == 1) x = A.ar.red1q(A.ar.shoup(x, A.rmod));
-        else x = fwd_to_canon<LAZY>(x, A);
+        const W x = fwd_to_canon<LAZY>(v[e], A);
         __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, e));
     }
 }
@@ -39,18 +38,26 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
     W v[G::E];
-    fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, in + poly * G::N, valid, A);
+    // fwd(a) * R (stage 0 scaled), so mont(fwd(a)R, w) = fwd(a) w; the raw
+    // lazy output (< (4+2L)q <= R) times a canonical w is a valid
+    // Montgomery pair.
+    fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     const uint64_t *wp = wv + poly * G::N;
     uint64_t *dst = out + poly * G::N;
-    const uint64_t wlim = (uint64_t)(W)~W(0);
+    // two chunks: 16 raw u64 w in flight at once would exceed 64 VGPRs
+    constexpr int CH = G::E >= 8 ? G::E / 8 : G::E;
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
-        // w * R mod q (Montgomery form) in [0, 2q); exact for any u64 w.
-        W wm = A.ar.mont(load_lazy<W>(__builtin_nontemporal_load(wp + gi), wlim, A.q64, A.mu64), A.ar.r2);
-        W x = A.ar.red1q(A.ar.mont(fwd_to_2q<LAZY>(v[e], A), wm));
-        __builtin_nontemporal_store((uint64_t)x, dst + gi);
+    for (int c0 = 0; c0 < G::E; c0 += CH) {
+        W w[CH];
+        load_coeffs<CH>(w, A.q64, A.q64, A.mu64, [&](int e) -> uint64_t {
+            return __builtin_nontemporal_load(wp + gidx<LOGN, G::NP - 1>(tau, c0 + e));
+        });
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            const W x = A.ar.red1q(A.ar.mont(v[c0 + e], w[e]));
+            __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, c0 + e));
+        }
     }
 }
 

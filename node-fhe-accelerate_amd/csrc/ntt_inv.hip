@@ -58,7 +58,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, a + poly * G::N, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
-        const W x = fwd_to_2q<LAZY>(v[e], A);
+        const W x = fwd_to_canon<LAZY>(v[e], A);  // canonical: times a raw output below
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);  // own positions: no sync needed
         if constexpr (STASH == 0) va[e] = x;
         else if constexpr (STASH == 1) st[gi] = x;
@@ -73,7 +73,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
         if constexpr (STASH == 0) x = va[e];
         else if constexpr (STASH == 1) x = st[gi];
         else x = valid ? (W)crow[gi] : W(0);
-        v[e] = A.ar.mont(x, fwd_to_2q<LAZY>(v[e], A));  // a*b*R^-1 in [0, 2q)
+        v[e] = A.ar.mont(x, v[e]);  // a*b*R^-1 in [0, 2q): canonical x raw v[e] (< R)
     }
     if constexpr (G::NP > 1) __syncthreads();
     inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tau, crow, valid, A, A.ninv_r, A.untwist_r);
