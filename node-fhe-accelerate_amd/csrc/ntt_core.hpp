@@ -60,9 +60,9 @@ struct Geo {
     // Waves per SIMD the LDS footprint allows (160 KiB LDS, 2048 threads per
     // CU): used as __launch_bounds__' min-waves-per-EU so the register
     // allocation never costs a resident workgroup.
-    template <typename W>
+    template <typename W, int EXTRA_WORDS = 0>
     static constexpr int occ_waves() {
-        const int by_lds = (160 * 1024) / (P * LW * (int)sizeof(W));
+        const int by_lds = (160 * 1024) / ((P * LW + EXTRA_WORDS) * (int)sizeof(W));
         const int by_thr = 2048 / THREADS;
         const int wg = by_lds < by_thr ? by_lds : by_thr;
         const int w = wg * THREADS / 64 / 4;

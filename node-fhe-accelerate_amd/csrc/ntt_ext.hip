@@ -18,35 +18,61 @@
 
 namespace FHE_NS {
 
+// Where the (k+1) NTT-domain accumulators live between rows: 1 = a second
+// LDS region, 2 = the ciphertext's own output rows in HBM (read-modify-write
+// of the thread's own positions; no synchronisation needed).  Holding them
+// in VGPRs spilled 300-800 B/lane.
+template <int LOGN, typename W, int K1>
+constexpr int ext_stash() {
+    using G = Geo<LOGN>;
+    return G::P * (G::LW + K1 * G::N) * (int)sizeof(W) <= 160 * 1024 ? 1 : 2;
+}
+template <int LOGN, typename W, int K1>
+constexpr int ext_extra_words() {
+    return ext_stash<LOGN, W, K1>() == 1 ? Geo<LOGN>::P * K1 * Geo<LOGN>::N : 0;
+}
+
+template <int LOGN, typename W, int K1>
+constexpr int ext_occ() {
+    constexpr int extra = ext_extra_words<LOGN, W, K1>();
+    return Geo<LOGN>::template occ_waves<W, extra>();
+}
+
 template <int LOGN, typename W, bool NEGA, int K1, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
-k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, uint64_t *__restrict__ out,
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ext_occ<LOGN, W, K1>()))
+k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, uint64_t *out,
           size_t batch, int level, int base_log, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::LW];
+    constexpr int STASH = ext_stash<LOGN, W, K1>();
+    __shared__ W lds_all[G::P * G::LW + ext_extra_words<LOGN, W, K1>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
-    W acc[K1][G::E];
-#pragma unroll
-    for (int j = 0; j < K1; ++j)
-#pragma unroll
-        for (int e = 0; e < G::E; ++e) acc[j][e] = 0;
+    uint64_t *orow = out + poly * K1 * G::N;
+    // accumulator j of this ciphertext: LDS, or row j of the output
+    auto acc = [&](int j) -> W * {
+        if constexpr (STASH == 1) return lds_all + G::P * G::LW + (pl * K1 + j) * G::N;
+        else return reinterpret_cast<W *>(orow + (size_t)j * G::N);
+    };
 
     const uint64_t base = 1ull << base_log, mask = base - 1, half = base / 2;
     const uint64_t q = A.q64, lim = (uint64_t)A.ar.q2 * 2;
     const int rows = K1 * level;
     for (int r = 0; r < rows; ++r) {
+        // opaque per-row copy of the lane index: keeps the (loop-invariant)
+        // address arithmetic inside the loop instead of 100+ hoisted VGPRs
+        uint32_t tr = tau;
+        asm volatile("" : "+v"(tr));
         const int i = r / level, l = r % level;
         const uint32_t shift = uint32_t(level - 1 - l) * uint32_t(base_log);
         const uint64_t *src = glwe + (poly * K1 + i) * G::N;
         if (r > 0 && G::NP > 1) __syncthreads();
         W v[G::E];
         Tw<W> t0[PassTw<LOGN, 0>::COUNT];
-        load_tw<LOGN, 0>(tau, A.twf, t0);
+        load_tw<LOGN, 0>(tr, A.twf, t0);
         load_coeffs<G::E>(v, lim, q, A.mu64, [&](int t) -> uint64_t {
-            const uint64_t c = valid ? src[tau + cbrv(t, G::LOGE) * G::T] : 0;
+            const uint64_t c = valid ? src[tr + cbrv(t, G::LOGE) * G::T] : 0;
             uint64_t d = (c >> shift) & mask;
             if (d > half) {
                 d = q - (base - d);
@@ -56,24 +82,48 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
         });
         if constexpr (NEGA) {
 #pragma unroll
-            for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tau + cbrv(t, G::LOGE) * G::T]);
+            for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tr + cbrv(t, G::LOGE) * G::T]);
         }
         fwd_pass<LOGN, 0, LAZY>(v, t0, A.ar);
-        fwd_rest<LOGN, 1, LAZY, kPfSingle>(lds, v, tau, A.twf, A.ar);
+        fwd_rest<LOGN, 1, LAZY, kPfSingle>(lds, v, tr, A.twf, A.ar);
+        if (!valid) continue;
         const uint64_t *g = ggsw + (size_t)r * K1 * G::N;
+        // chunks of 2 coefficients: all key + accumulator loads of the row in
+        // flight at once would not fit the register budget
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) {
-            const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
-            const W d = v[e];  // raw output (< R) times a canonical key: valid Montgomery pair
+        for (int c0 = 0; c0 < G::E; c0 += 2) {
+            uint64_t kv[2][K1];
+            W pv[2][K1];
 #pragma unroll
-            for (int j = 0; j < K1; ++j)
-                acc[j][e] = A.ar.red2q(acc[j][e] + A.ar.mont(d, (W)g[(size_t)j * G::N + gi]));
+            for (int e = 0; e < 2; ++e)
+#pragma unroll
+                for (int j = 0; j < K1; ++j) {
+                    const uint32_t gi = gidx<LOGN, G::NP - 1>(tr, c0 + e);
+                    kv[e][j] = g[(size_t)j * G::N + gi];
+                    pv[e][j] = r == 0 ? W(0) : acc(j)[gi];
+                }
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+#pragma unroll
+                for (int j = 0; j < K1; ++j) {
+                    // raw output (< R) times a canonical key: valid Montgomery pair
+                    const W m = A.ar.mont(v[c0 + e], (W)kv[e][j]);
+                    acc(j)[gidx<LOGN, G::NP - 1>(tr, c0 + e)] = A.ar.red2q(pv[e][j] + m);
+                }
         }
     }
-#pragma unroll
+#pragma nounroll
     for (int j = 0; j < K1; ++j) {
         if (G::NP > 1) __syncthreads();
-        inv_poly_from_regs<LOGN, NEGA>(lds, acc[j], tau, out + (poly * K1 + j) * G::N, valid, A, A.ninv, A.untwist);
+        uint32_t tr = tau;
+        asm volatile("" : "+v"(tr));
+        W v[G::E];
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) v[e] = valid ? acc(j)[gidx<LOGN, G::NP - 1>(tr, e)] : W(0);
+        if constexpr (STASH == 2) {
+            if (G::NP > 1) __syncthreads();  // every stash read of row j precedes its final stores
+        }
+        inv_poly_from_regs<LOGN, NEGA>(lds, v, tr, orow + (size_t)j * G::N, valid, A, A.ninv, A.untwist);
     }
 }
 

@@ -33,15 +33,24 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 // full and the kernel is ALU-bound, so 16N extra bytes are cheap).  Keeping
 // both spectra in VGPRs cost 150-255 VGPRs (N <= 8192) or scratch spills
 // (N = 16384).
+#ifndef FHE_POLY_HBM_STASH
+#define FHE_POLY_HBM_STASH 0
+#endif
 template <int LOGN, typename W>
 constexpr int polymul_stash() {
     using G = Geo<LOGN>;
     if (LOGN < 5) return 0;
+    if (FHE_POLY_HBM_STASH && LOGN == 14) return 2;
     return G::P * (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024 ? 1 : 2;
+}
+template <int LOGN, typename W>
+constexpr int polymul_occ() {
+    // with the stash in HBM the LDS footprint admits a second workgroup
+    return polymul_stash<LOGN, W>() == 2 && FHE_POLY_HBM_STASH ? Geo<LOGN>::template occ_waves<W>() : 1;
 }
 
 template <int LOGN, typename W, bool NEGA, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS)
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
 k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
           NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -65,10 +74,15 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
         else if (valid) crow[gi] = (uint64_t)x;
     }
     if constexpr (G::NP > 1) __syncthreads();  // LDS exchange buffer is reused by the second transform
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, b + poly * G::N, valid, A);
+    // opaque copy of the lane index (u64 path): stops the compiler from
+    // keeping the first transform's address arithmetic live for reuse.  At
+    // u32 the reuse is cheaper than recomputing (measured, r05 A/B).
+    uint32_t tb = tau;
+    if constexpr (sizeof(W) == 8) asm volatile("" : "+v"(tb));
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
-        const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tb, e);
         W x;
         if constexpr (STASH == 0) x = va[e];
         else if constexpr (STASH == 1) x = st[gi];
@@ -76,7 +90,9 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
         v[e] = A.ar.mont(x, v[e]);  // a*b*R^-1 in [0, 2q): canonical x raw v[e] (< R)
     }
     if constexpr (G::NP > 1) __syncthreads();
-    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tau, crow, valid, A, A.ninv_r, A.untwist_r);
+    uint32_t ti = tau;
+    if constexpr (sizeof(W) == 8) asm volatile("" : "+v"(ti));
+    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, ti, crow, valid, A, A.ninv_r, A.untwist_r);
 }
 
 template <int LOGN, typename W, bool NEGA>

@@ -29,11 +29,19 @@ for q in [int(x) for x in args.qs.split(",")]:
     b = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
     out = torch.empty_like(a)
     ring = fhe_gpu.PolynomialRing(n, q)
+    eps = {}
+    for bl, lv in ((23, 1), (15, 2)):
+        ggsw = torch.randint(0, q, (2 * lv, 2, n), device="cuda", dtype=torch.int64, generator=g)
+        eps[lv] = fhe_gpu.ExternalProduct(ring, ggsw, bl, lv)
+    glwe = a[: B // 2].view(B // 4, 2, n)  # B/4 ciphertexts (k = 1)
+    gout = out[: B // 2].view(B // 4, 2, n)
     for op in args.ops.split(","):
         fn = {"fwd_mul": lambda: ring.forward_ntt_mul(a, b, out=out),
               "polymul": lambda: ring.multiply(a, b, out=out),
               "fwd": lambda: ring.forward_ntt(a, out=out),
-              "inv": lambda: ring.inverse_ntt(a, out=out)}[op]
+              "inv": lambda: ring.inverse_ntt(a, out=out),
+              "ext1": lambda: eps[1](glwe, out=gout),
+              "ext2": lambda: eps[2](glwe, out=gout)}[op]
         fn()
         torch.cuda.synchronize()
         chk = int(out[:8].sum().item()) ^ int(out[-8:].sum().item())
