@@ -80,8 +80,10 @@ int fhe_detect(fhe_hw_caps *caps);
 /* ---- context: NTTProcessor(degree, modulus) + PolynomialRing(degree, q)
  * (ntt_processor.cpp:134-208, polynomial_ring.cpp:213-222).
  * Validation order and messages follow the reference constructor.  n must
- * be a power of two in [4, 65536]; the GPU kernels currently implement
- * n <= 16384 and q < 2^62 (FHE_ERR_UNSUPPORTED otherwise).
+ * be a power of two in [4, 65536]; the GPU kernels implement every such n
+ * and q < 2^62 (FHE_ERR_UNSUPPORTED otherwise).  n > 16384 runs as a
+ * two-pass row/column split and the context holds 512 MiB of device
+ * scratch; the external product is limited to n <= 16384.
  * device: HIP device ordinal.                                              */
 int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out);
 void fhe_ctx_destroy(fhe_ctx *ctx);

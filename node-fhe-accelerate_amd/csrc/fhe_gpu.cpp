@@ -188,6 +188,8 @@ void free_tables(fhe_ctx *c) {
     c->tab = Tables{};
     for (auto &s : c->scratch)
         if (s) { (void)hipFree(s); s = nullptr; }
+    for (auto &s : c->plan.big_scratch)
+        if (s) { (void)hipFree(s); s = nullptr; }
 }
 
 FHE_NS::ModConsts mod_consts(u64 q) {
@@ -327,6 +329,14 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     }
     DeviceGuard g(device);
     int rc = c->word == 32 ? build_tables<u32>(c, c->plan.a32) : build_tables<u64>(c, c->plan.a64);
+    if (rc == FHE_OK && (int)logn > FHE_NS::kMaxFusedLogN) {
+        // two-pass transforms (ntt_big.hip): 2 x 256 MiB of chunk scratch
+        c->plan.big_chunk = ((size_t)1 << 25) >> logn;
+        for (auto &sp : c->plan.big_scratch) {
+            hipError_t e = hipMalloc((void **)&sp, c->plan.big_chunk * n * sizeof(u64));
+            if (e != hipSuccess) { rc = hip_fail(e, "hipMalloc(big-N scratch)"); break; }
+        }
+    }
     if (rc == FHE_OK) {
         hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
         if (e != hipSuccess) rc = hip_fail(e, "hipStreamCreate");
@@ -375,7 +385,7 @@ int fhe_ctx_get_info(const fhe_ctx *c, fhe_ctx_info *info) {
     info->n = c->n; info->log_n = c->logn; info->q = c->q; info->psi = c->psi; info->psi_inv = c->psi_inv;
     info->inv_n = c->inv_n; info->mode = c->mode; info->word_bits = c->word; info->device = c->device;
     const int loge = c->logn < 4 ? (int)c->logn : 4;
-    const int t = 1 << (c->logn - loge);
+    const int t = 1 << ((c->logn > (u32)FHE_NS::kMaxFusedLogN ? (u32)FHE_NS::kMaxFusedLogN : c->logn) - loge);
     info->polys_per_block = t >= 256 ? 1 : 256 / t;
     info->threads_per_block = t * info->polys_per_block;
     return FHE_OK;
@@ -453,7 +463,9 @@ int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, ui
     });
 }
 
-static int check_decomp(uint32_t k, uint32_t base_log, uint32_t level) {
+static int check_decomp(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level) {
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN)
+        return fail(FHE_ERR_UNSUPPORTED, "external product implemented for degrees up to 16384");
     if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
     if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
         return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
@@ -462,6 +474,8 @@ static int check_decomp(uint32_t k, uint32_t base_log, uint32_t level) {
 
 int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggsw, uint64_t *ggsw_ntt, int where) {
     if (int rc = check_ctx(c)) return rc;
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN)
+        return fail(FHE_ERR_UNSUPPORTED, "external product implemented for degrees up to 16384");
     if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
     if (level == 0) return fail(FHE_ERR_INVALID_ARG, "level must be >= 1");
     const size_t polys = (size_t)(k + 1) * level * (k + 1);
@@ -472,7 +486,7 @@ int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggs
 int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
                                const uint64_t *ggsw_ntt, uint64_t *out, size_t batch, int where) {
     if (int rc = check_ctx(c)) return rc;
-    if (int rc = check_decomp(k, base_log, level)) return rc;
+    if (int rc = check_decomp(c, k, base_log, level)) return rc;
     if (!ggsw_ntt && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const size_t per = (size_t)(k + 1) * c->n;
     if (where == FHE_HOST && batch) {

@@ -15,12 +15,16 @@ struct Plan {
     int nega;   // 0 = compat, 1 = negacyclic
     int lazy;   // 32-bit path with (4 + 2L) q <= 2^32: forward stages skip reductions
     hipStream_t stream;
+    // N > 2^kMaxFusedLogN (ntt_big.hip): two chunk-sized scratch buffers
+    uint64_t *big_scratch[2];
+    size_t big_chunk;  // polynomials per scratch chunk
     NttArgs<uint32_t> a32;
     NttArgs<uint64_t> a64;
 };
 
 constexpr int kMinLogN = 2;
-constexpr int kMaxLogN = 14;
+constexpr int kMaxFusedLogN = 14;  // one workgroup per polynomial up to here
+constexpr int kMaxLogN = 16;       // NTTProcessor's limit (ntt_processor.cpp:146)
 
 // Forward NTT; epi 0: canonical output, 1: output * R mod q (Montgomery
 // form, used to prepare GGSW keys).
@@ -30,6 +34,8 @@ hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t b
 hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch);
 // c = inv(fwd(a) (.) fwd(b))  (PolynomialRing::multiply)
 hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
+// N > 2^kMaxFusedLogN: op 0 fwd, 1 fwd*R, 2 fwd (.) b, 3 inv, 4 polymul
+hipError_t launch_big(const Plan &p, int op, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
 // TFHE external product, GGSW already in NTT-Montgomery form.
 hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const uint64_t *glwe,
                           const uint64_t *ggsw, uint64_t *out, size_t batch);

@@ -310,20 +310,26 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
 // values in [0, 4q), or [0, (4+2L)q) when LAZY; every bound is <= R, so a
 // raw output times a canonical residue is a valid Montgomery operand pair).
 // RS: the result is the transform times R (Montgomery form).
+//
+// Sub-transform use (N > 16384, ntt_big.hip): the 2^LOGN coefficients are
+// the strided subsequence src[i << sh] of a larger polynomial whose element
+// src[0] has global index `off` (twist table index (i << sh) | off); the
+// prefix stages of the big transform use the same stage-major twiddles.
 template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, bool RS = false, typename W>
 __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const uint64_t *__restrict__ src,
-                                         bool valid, const NttArgs<W> &A) {
+                                         bool valid, const NttArgs<W> &A, uint32_t sh = 0, uint32_t off = 0) {
     using G = Geo<LOGN>;
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
     load_tw<LOGN, 0>(tau, A.twf, t0);
     // Shoup-based first steps (twist / R-scaling) accept any word
     const uint64_t lim = (NEGA || RS) ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
-        return valid ? __builtin_nontemporal_load(src + tau + cbrv(t, G::LOGE) * G::T) : 0;
+        return valid ? __builtin_nontemporal_load(src + ((tau + cbrv(t, G::LOGE) * G::T) << sh)) : 0;
     });
     if constexpr (NEGA) {
 #pragma unroll
-        for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tau + cbrv(t, G::LOGE) * G::T]);
+        for (int t = 0; t < G::E; ++t)
+            v[t] = A.ar.shoup(v[t], A.twist[((tau + cbrv(t, G::LOGE) * G::T) << sh) | off]);
     }
     fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
     fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar);
@@ -332,10 +338,12 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
 // Inverse transform from v (last-pass layout, values in [0, 2q)) to HBM
 // (bit-reversed store, coalesced), canonical output.  scale = N^-1 or
 // N^-1 * R; post = the matching negacyclic post-twist table.
+// Sub-transform use (ntt_big.hip): output i goes to dst[i << sh], global
+// index (i << sh) | off for the post-twist.
 template <int LOGN, bool NEGA, int PF = kPfSingle, typename W>
 __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, uint64_t *__restrict__ dst,
                                                    bool valid, const NttArgs<W> &A, Tw<W> scale,
-                                                   const Tw<W> *__restrict__ post) {
+                                                   const Tw<W> *__restrict__ post, uint32_t sh = 0, uint32_t off = 0) {
     using G = Geo<LOGN>;
     constexpr int LAST = G::NP - 1;
     {
@@ -346,9 +354,9 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
     inv_rest<LOGN, LAST - 1, !NEGA, PF>(lds, v, tau, A.twi, A.ar, scale);
 #pragma unroll
     for (int t = 0; t < G::E; ++t) {
-        const uint32_t gi = tau + cbrv(t, G::LOGE) * G::T;
+        const uint32_t gi = (tau + cbrv(t, G::LOGE) * G::T) << sh;
         W x = v[t];
-        if constexpr (NEGA) x = A.ar.shoup(x, post[gi]);
+        if constexpr (NEGA) x = A.ar.shoup(x, post[gi | off]);
         if (valid) __builtin_nontemporal_store((uint64_t)A.ar.red1q(x), dst + gi);
     }
 }

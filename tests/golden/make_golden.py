@@ -39,7 +39,7 @@ Q2048 = 40961  # 10*4096 + 1, prime
 
 SMALL = [(8, 17), (16, 97), (32, 193), (64, 257), (128, 769), (256, 7681), (512, 12289),
          (1024, P27), (1024, P62), (2048, Q2048), (4096, P27)]
-LARGE = [(4096, P62), (16384, P27), (16384, P62)]
+LARGE = [(4096, P62), (16384, P27), (16384, P62), (32768, P27), (32768, P62), (65536, P27), (65536, P62)]
 
 
 def L(a):

@@ -59,7 +59,7 @@ def test_version_and_detect():
         (131072, 97, -2, "Polynomial degree must be between 4 and 65536"),
         (8, 96, -3, "Modulus must be odd"),
         (16, 17, -4, "Modulus is not NTT-friendly"),
-        (32768, 65537, -10, "degrees up to 16384"),
+        (8, 4611686018428108801, -10, "moduli below 2^62"),  # q > 2^62, NTT-friendly
     ],
 )
 def test_ctx_validation_messages(n, q, code, msg):

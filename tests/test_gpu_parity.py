@@ -79,14 +79,15 @@ def test_golden_large(fg, golden_dir):
 # ------------------------------------------------------------ oracle sweeps
 CONFIGS = [(4, 17), (8, 17), (16, 97), (32, 193), (64, 257), (128, 769), (256, 7681), (512, 12289),
            (1024, P27), (1024, P62), (2048, 40961), (4096, P27), (4096, P62), (8192, P27), (8192, P62),
-           (16384, P27), (16384, P62), (1024, 1152921504606584833), (2048, 1073479681)]
+           (16384, P27), (16384, P62), (1024, 1152921504606584833), (2048, 1073479681),
+           (32768, P27), (32768, P62), (65536, P27), (65536, P62)]
 
 
 @pytest.mark.parametrize("n,q", CONFIGS)
 def test_transforms_vs_oracle(fg, n, q):
     r = fg.PolynomialRing(n, q)
     t = oracle.NTT(n, q)
-    b = 5 if n >= 4096 else 37  # ragged: not a multiple of polys-per-block
+    b = 3 if n > 16384 else 5 if n >= 4096 else 37  # ragged: not a multiple of polys-per-block
     x = oracle.splitmix_fill(n * 31 + 1, q, b * n).reshape(b, n)
     y = oracle.splitmix_fill(n * 31 + 2, q, b * n).reshape(b, n)
     assert (r.forward_ntt(x) == t.forward(x)).all()
@@ -96,7 +97,8 @@ def test_transforms_vs_oracle(fg, n, q):
     assert (r.pointwise_multiply(x, y) == oracle.pointwise(q, x.ravel(), y.ravel()).reshape(b, n)).all()
 
 
-@pytest.mark.parametrize("n,q", [(64, 257), (1024, P27), (1024, P62), (16384, P27), (16384, P62)])
+@pytest.mark.parametrize("n,q", [(64, 257), (1024, P27), (1024, P62), (16384, P27), (16384, P62), (32768, P27),
+                                 (65536, P62)])
 def test_non_canonical_inputs(fg, n, q):
     """Inputs are any u64 and behave as x mod q (the reference reduces in
     mod_add/mod_sub and the 128-bit %)."""
@@ -173,6 +175,42 @@ def test_round_trip_full_config_sizes(fg):
         t = oracle.NTT(n, q)
         xs = x[rows].cpu().numpy().view(np.uint64)
         assert (f[rows].cpu().numpy().view(np.uint64) == t.forward(xs)).all()
+
+
+def test_large_degree_chunk_boundaries(fg):
+    """N > 16384 runs as two passes over ctx-owned scratch in chunks of
+    2^25 / N polynomials (ntt_big.hip): batches that straddle a chunk and
+    the XCD grouping (multiples of 8) must not matter.  Rows around the
+    boundary are checked against the oracle, the rest by properties."""
+    import torch
+
+    for n, q, b in ((65536, P27, 514), (32768, P62, 1027)):
+        chunk = (1 << 25) // n
+        r = fg.PolynomialRing(n, q)
+        g = torch.Generator(device="cuda").manual_seed(n + b)
+        x = torch.randint(0, q, (b, n), device="cuda", dtype=torch.int64, generator=g)
+        y = torch.roll(x, 1, 0)
+        f = r.forward_ntt(x)
+        assert torch.equal(r.inverse_ntt(f), x)
+        m = r.multiply(x, y)
+        fm = r.forward_ntt_mul(x, y)
+        rows = [0, 7, chunk - 1, chunk, chunk + 1, b - 1]
+        t = oracle.NTT(n, q)
+        xs = x[rows].cpu().numpy().view(np.uint64)
+        ys = y[rows].cpu().numpy().view(np.uint64)
+        assert (f[rows].cpu().numpy().view(np.uint64) == t.forward(xs)).all()
+        assert (m[rows].cpu().numpy().view(np.uint64) == t.polymul(xs, ys)).all()
+        assert (fm[rows].cpu().numpy().view(np.uint64) == t.fwd_mul(xs, ys)).all()
+        # in place (out aliases an input) goes through the scratch as well
+        r.multiply(x, y, out=x)
+        assert torch.equal(x, m)
+
+
+def test_large_degree_external_product_unsupported(fg):
+    r = fg.PolynomialRing(32768, P62)
+    with pytest.raises(fg.FHEError) as ei:
+        fg.ExternalProduct(r, np.zeros((2, 2, 32768), np.uint64), 23, 1)
+    assert ei.value.code == -10
 
 
 # ------------------------------------------------------------ ring elementwise
@@ -284,7 +322,7 @@ def test_negacyclic_mode_is_ring_product(fg, golden_dir):
         assert L(r.multiply(U(c["x"]), U(c["y"]))) == c["product"]
     # larger: schoolbook via the oracle's exact integer arithmetic is too slow,
     # check the convolution identity x * X == shift with sign
-    for n, q in ((4096, P62), (16384, P27)):
+    for n, q in ((4096, P62), (16384, P27), (32768, P62), (65536, P27)):
         r = fg.PolynomialRing(n, q, mode="negacyclic")
         x = oracle.splitmix_fill(3, q, n).reshape(1, n)
         X = np.zeros((1, n), np.uint64)

@@ -167,6 +167,20 @@ def test_oracle_matches_pyref(n, q):
     assert [int(v) for v in t.polymul(x, y)] == pyref.polymul(xs, ys, q)
 
 
+@pytest.mark.parametrize("n,q", [(32768, P62), (65536, P27)])
+def test_oracle_matches_pyref_large_degree(n, q):
+    """The degrees the two-pass GPU path serves: N = 32768 with the 62-bit
+    prime is the TS round-trip suite's largest case
+    (ntt-round-trip.prop.test.ts:43); 65536 is NTTProcessor's maximum
+    (ntt_processor.cpp:146)."""
+    t = oracle.NTT(n, q)
+    x = oracle.splitmix_fill(n + 5, q, n)
+    xs = [int(v) for v in x]
+    f = t.forward(x)
+    assert [int(v) for v in f] == pyref.forward(xs, q)
+    assert (t.inverse(f) == x).all()
+
+
 def test_non_canonical_inputs_behave_mod_q():
     t = oracle.NTT(64, 257)
     x = np.random.default_rng(2).integers(0, 2 ** 64 - 1, 64, dtype=np.uint64, endpoint=True)
