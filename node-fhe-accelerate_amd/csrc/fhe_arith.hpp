@@ -41,7 +41,22 @@ struct Arith {
 #ifndef FHE_SHOUP_MAD
 #define FHE_SHOUP_MAD 1
 #endif
-        if constexpr (sizeof(W) == 4 && FHE_SHOUP_MAD) {
+#ifndef FHE_SHOUP_ASM
+#define FHE_SHOUP_ASM 1
+#endif
+        if constexpr (sizeof(W) == 4 && FHE_SHOUP_ASM) {
+            // One v_mad_u64_u32 for x*w - h*q (mod 2^32): LLVM narrows the
+            // 64-bit form below to two v_mul_lo_u32 + v_sub.  Only the low
+            // half of the addend matters, so its high half is left undefined
+            // (no zeroing move).
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            u32x2 c;
+            c.x = x * w;
+            uint64_t r, cy;
+            asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "v"(h), "s"(0u - q), "v"(c));
+            (void)cy;
+            return (W)r;
+        } else if constexpr (sizeof(W) == 4 && FHE_SHOUP_MAD) {
             // x*w - h*q (mod 2^32) as one v_mad_u64_u32: h*(2^32 - q) + x*w
             return (W)((uint64_t)h * (uint32_t)(0u - q) + (uint32_t)(x * w));
         } else {

@@ -52,14 +52,14 @@ k_big_fwd_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size
     uint32_t b;
     big_map<M>(poly, b);
     const bool valid = poly < batch;
+    if (!valid) return;  // whole workgroup (P == 1)
     const uint32_t tau = threadIdx.x, o = cbrv(b, M);
     W v[G::E];
     fwd_poly<kBigS, NEGA, LAZY>(lds, v, tau, in + (poly << (kBigS + M)) + o, valid, A, M, o);
-    if (!valid) return;
-    uint64_t *dst = out + (poly << (kBigS + M)) + ((size_t)b << kBigS);
+    const auto r = brsrc(out + (poly << (kBigS + M)) + ((size_t)b << kBigS));
+    const uint32_t vo = LastIO<kBigS>::vo(tau);
 #pragma unroll
-    for (int e = 0; e < G::E; ++e)
-        __builtin_nontemporal_store((uint64_t)fwd_to_canon<LAZY>(v[e], A), dst + gidx<kBigS, G::NP - 1>(tau, e));
+    for (int e = 0; e < G::E; ++e) bstore(r, vo, LastIO<kBigS>::so(e), (uint64_t)fwd_to_canon<LAZY>(v[e], A));
 }
 
 template <int M, typename W, bool NEGA, bool MONT>
@@ -71,14 +71,13 @@ k_big_inv_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size
     uint32_t b;
     big_map<M>(poly, b);
     const bool valid = poly < batch;
+    if (!valid) return;  // whole workgroup (P == 1)
     const uint32_t tau = threadIdx.x, o = cbrv(b, M);
-    const uint64_t *src = in + (poly << (kBigS + M)) + ((size_t)b << kBigS);
+    const auto r = brsrc(in + (poly << (kBigS + M)) + ((size_t)b << kBigS));
+    const uint32_t vo = LastIO<kBigS>::vo(tau);
     W v[G::E];
-#pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const uint64_t x = valid ? __builtin_nontemporal_load(src + gidx<kBigS, G::NP - 1>(tau, e)) : 0;
-        v[e] = load_lazy<W>(x, (uint64_t)A.ar.q2, A.q64, A.mu64);
-    }
+    load_coeffs<G::E>(v, (uint64_t)A.ar.q2, A.q64, A.mu64,
+                      [&](int e) -> uint64_t { return bload(r, vo, LastIO<kBigS>::so(e)); });
     inv_poly_from_regs<kBigS, NEGA>(lds, v, tau, out + (poly << (kBigS + M)) + o, valid, A,
                                     MONT ? A.ninv_r : A.ninv, MONT ? A.untwist_r : A.untwist, M, o);
 }

@@ -130,6 +130,58 @@ __device__ __forceinline__ uint32_t gidx(uint32_t tau, int e) {
     return lay<S, R>(g_of<LOGN, PASS>(tau, u)) | (uint32_t(t) << S);
 }
 
+// gidx = gidx_var(tau) + gidx_const(e) for PASS > 0: g = tau | (u << LOGT)
+// has disjoint bit fields and lay() only moves bit fields, so the lane part
+// and the slot part add without carries.
+template <int LOGN, int PASS>
+__device__ __forceinline__ uint32_t gidx_var(uint32_t tau) {
+    static_assert(PASS > 0, "pass 0 is bit-reversed");
+    using G = Geo<LOGN>;
+    return lay<G::S(PASS), G::R(PASS)>(tau);
+}
+template <int LOGN, int PASS>
+__host__ __device__ constexpr uint32_t gidx_const(int e) {
+    using G = Geo<LOGN>;
+    constexpr int S = G::S(PASS), R = G::R(PASS);
+    const uint32_t t = uint32_t(e) & ((1u << R) - 1), u = uint32_t(e) >> R;
+    const uint32_t g = u << G::LOGT;
+    return ((g & ((1u << S) - 1)) | ((g >> S) << (S + R))) | (t << S);
+}
+
+// ---------------------------------------------------------------- HBM I/O
+// Buffer loads/stores through a workgroup-uniform resource (used when a
+// workgroup owns one polynomial, P == 1): the lane's byte offset is shared by
+// all E accesses of a layout and each access adds a compile-time constant in
+// an SGPR, so no 64-bit VALU address arithmetic is issued per access.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kAuxNT = 2;  // gfx950 cache policy bit 'nt': streamed once
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)0xFFFFFFFF, 0x00020000);
+}
+template <int AUX = kAuxNT>
+__device__ __forceinline__ uint64_t bload(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, AUX));
+}
+template <int AUX = kAuxNT>
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, uint64_t x) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, x), r, vo, so, AUX);
+}
+template <typename W>
+__device__ __forceinline__ Tw<W> bload_tw(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    if constexpr (sizeof(W) == 4)
+        return __builtin_bit_cast(Tw<W>, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+    else
+        return __builtin_bit_cast(Tw<W>, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+}
+// Last-pass (natural order) coefficient access of a P == 1 polynomial.
+template <int LOGN>
+struct LastIO {
+    static constexpr int PASS = Geo<LOGN>::NP - 1;
+    __device__ static uint32_t vo(uint32_t tau) { return gidx_var<LOGN, PASS>(tau) * 8u; }
+    static constexpr uint32_t so(int e) { return gidx_const<LOGN, PASS>(e) * 8u; }
+};
+
 // ---------------------------------------------------------------- twiddles
 // Twiddles of one pass, loaded into VGPRs ahead of use: slot (k, u, tl) is
 // butterfly group tl of global stage S+k for slot-group u.  The loads of
@@ -149,12 +201,16 @@ struct PassTw {
 // on MI355X: 2 for the single-transform kernels (64-VGPR budget at two
 // workgroups per CU), 4 for polymul (one workgroup per CU).
 constexpr int kPfSingle = 2;
-constexpr int kPfPolymul = 4;
+#ifndef FHE_PF_POLYMUL
+#define FHE_PF_POLYMUL 4
+#endif
+constexpr int kPfPolymul = FHE_PF_POLYMUL;
 
 template <int LOGN, int PASS, typename W, int K0 = 0, int K1 = 8>
 __device__ __forceinline__ void load_tw(uint32_t tau, const Tw<W> *__restrict__ tw,
                                         Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT]) {
     using P = PassTw<LOGN, PASS>;
+    using G = Geo<LOGN>;
     constexpr int S = P::S, R = P::R, NU = P::NU;
     constexpr int KE = K1 < R ? K1 : R;
 #pragma unroll
@@ -169,6 +225,12 @@ __device__ __forceinline__ void load_tw(uint32_t tau, const Tw<W> *__restrict__ 
                     typedef const __attribute__((address_space(4))) W cw_t;
                     const cw_t *cp = (const cw_t *)(const void *)tw;
                     t[P::slot(k, u, tl)] = Tw<W>{cp[2 * idx], cp[2 * idx + 1]};
+                } else if constexpr (G::P == 1) {
+                    // idx = (tau & m) + const: jlo = (tau | u << LOGT) & m, disjoint fields
+                    constexpr uint32_t m = (1u << S) - 1;
+                    const uint32_t cst = (1u << (S + k)) + ((uint32_t(u) << G::LOGT) & m) + (uint32_t(tl) << S);
+                    t[P::slot(k, u, tl)] = bload_tw<W>(brsrc(tw), (tau & m) * (uint32_t)sizeof(Tw<W>),
+                                                       cst * (uint32_t)sizeof(Tw<W>));
                 } else
                     t[P::slot(k, u, tl)] = tw[idx];
             }
@@ -220,10 +282,18 @@ __device__ __forceinline__ void inv_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[
             }
 }
 
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
 // Passes PASS..NP-1 of the forward transform, exchanging through LDS.
-template <int LOGN, int PASS, bool LAZY, int PF, typename W>
+// hook() runs once, in the last pass after its twiddle loads are issued: the
+// place to start HBM loads for what follows the transform (VMEM counters
+// retire in order, so loads issued earlier would make every later twiddle
+// wait for them).
+template <int LOGN, int PASS, bool LAZY, int PF, typename W, typename H = NoHook>
 __device__ __forceinline__ void fwd_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const Tw<W> *__restrict__ tw,
-                                         const Arith<W> &ar) {
+                                         const Arith<W> &ar, H &&hook = NoHook{}) {
     using G = Geo<LOGN>;
     if constexpr (PASS < G::NP) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
@@ -232,8 +302,9 @@ __device__ __forceinline__ void fwd_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
         __syncthreads();
         lds_load<LOGN, PASS>(lds, v, tau);
         load_tw<LOGN, PASS, W, PF, 8>(tau, tw, t);
+        if constexpr (PASS == G::NP - 1) hook();
         fwd_pass<LOGN, PASS, LAZY>(v, t, ar);
-        fwd_rest<LOGN, PASS + 1, LAZY, PF>(lds, v, tau, tw, ar);
+        fwd_rest<LOGN, PASS + 1, LAZY, PF>(lds, v, tau, tw, ar, hook);
     }
 }
 
@@ -287,6 +358,19 @@ __device__ __forceinline__ W fwd_to_canon(W x, const NttArgs<W> &A) {
 // E coefficients of one polynomial from HBM into the lazy range [0, lim) of
 // word W.  Out-of-range inputs (any u64 behaves as x mod q) take one
 // divergent slow path for the whole thread.
+template <int E, typename W>
+__device__ __forceinline__ void coeffs_from_raw(W (&v)[E], uint64_t (&raw)[E], uint64_t lim, uint64_t q, uint64_t mu) {
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < E; ++t) bad |= raw[t] >= lim;
+    if (__builtin_expect(bad, 0)) {
+#pragma unroll
+        for (int t = 0; t < E; ++t)
+            if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+    }
+#pragma unroll
+    for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
+}
 template <int E, typename W, typename F>
 __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q, uint64_t mu, F &&addr_of) {
     uint64_t raw[E];
@@ -315,24 +399,44 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
 // the strided subsequence src[i << sh] of a larger polynomial whose element
 // src[0] has global index `off` (twist table index (i << sh) | off); the
 // prefix stages of the big transform use the same stage-major twiddles.
-template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, bool RS = false, typename W>
+// Raw pass-0 coefficients of a P == 1 polynomial (bit-reversed order), for
+// prefetching through a fwd_rest hook.
+template <int LOGN>
+__device__ __forceinline__ void load_raw(uint64_t (&raw)[Geo<LOGN>::E], uint32_t tau, const uint64_t *src) {
+    using G = Geo<LOGN>;
+    const auto r = brsrc(src);
+#pragma unroll
+    for (int t = 0; t < G::E; ++t) raw[t] = bload(r, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u);
+}
+template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, bool RS = false, typename W, typename H = NoHook>
 __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const uint64_t *__restrict__ src,
-                                         bool valid, const NttArgs<W> &A, uint32_t sh = 0, uint32_t off = 0) {
+                                         bool valid, const NttArgs<W> &A, uint32_t sh = 0, uint32_t off = 0,
+                                         H &&hook = NoHook{}, uint64_t (*pre)[Geo<LOGN>::E] = nullptr) {
     using G = Geo<LOGN>;
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
     load_tw<LOGN, 0>(tau, A.twf, t0);
     // Shoup-based first steps (twist / R-scaling) accept any word
     const uint64_t lim = (NEGA || RS) ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
-    load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
-        return valid ? __builtin_nontemporal_load(src + ((tau + cbrv(t, G::LOGE) * G::T) << sh)) : 0;
-    });
+    if (pre) {  // prefetched by the caller (load_raw)
+        coeffs_from_raw<G::E>(v, *pre, lim, A.q64, A.mu64);
+    } else if constexpr (G::P == 1) {  // the caller has returned early if !valid
+        const auto r = brsrc(src);
+        const uint32_t vo = (tau << sh) * 8u;
+        load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+            return bload(r, vo, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u);
+        });
+    } else {
+        load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+            return valid ? __builtin_nontemporal_load(src + ((tau + cbrv(t, G::LOGE) * G::T) << sh)) : 0;
+        });
+    }
     if constexpr (NEGA) {
 #pragma unroll
         for (int t = 0; t < G::E; ++t)
             v[t] = A.ar.shoup(v[t], A.twist[((tau + cbrv(t, G::LOGE) * G::T) << sh) | off]);
     }
     fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
-    fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar);
+    fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar, hook);
 }
 
 // Inverse transform from v (last-pass layout, values in [0, 2q)) to HBM
@@ -357,7 +461,10 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
         const uint32_t gi = (tau + cbrv(t, G::LOGE) * G::T) << sh;
         W x = v[t];
         if constexpr (NEGA) x = A.ar.shoup(x, post[gi | off]);
-        if (valid) __builtin_nontemporal_store((uint64_t)A.ar.red1q(x), dst + gi);
+        if constexpr (G::P == 1)
+            bstore(brsrc(dst), (tau << sh) * 8u, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u, (uint64_t)A.ar.red1q(x));
+        else if (valid)
+            __builtin_nontemporal_store((uint64_t)A.ar.red1q(x), dst + gi);
     }
 }
 

@@ -48,6 +48,7 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
+    if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped
     W *lds = lds_all + pl * G::LW;
     uint64_t *orow = out + poly * K1 * G::N;
     // accumulator j of this ciphertext: LDS, or row j of the output

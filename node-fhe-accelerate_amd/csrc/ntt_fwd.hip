@@ -15,18 +15,29 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
+    if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped
     W v[G::E];
     // EPI 1: transform times R (Montgomery form), folded into stage 0
     fwd_poly<LOGN, NEGA, LAZY, kPfSingle, EPI == 1>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     uint64_t *dst = out + poly * G::N;
+    if constexpr (G::P == 1) {
+        const auto r = brsrc(dst);
+        const uint32_t vo = LastIO<LOGN>::vo(tau);
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        const W x = fwd_to_canon<LAZY>(v[e], A);
-        __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, e));
+        for (int e = 0; e < G::E; ++e) bstore(r, vo, LastIO<LOGN>::so(e), (uint64_t)fwd_to_canon<LAZY>(v[e], A));
+    } else {
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const W x = fwd_to_canon<LAZY>(v[e], A);
+            __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, e));
+        }
     }
 }
 
+#ifndef FHE_FWDMUL_PREFETCH
+#define FHE_FWDMUL_PREFETCH 1
+#endif
 template <int LOGN, typename W, bool NEGA, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
@@ -37,26 +48,56 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
+    if (G::P == 1 && !valid) return;
     W v[G::E];
     // fwd(a) * R (stage 0 scaled), so mont(fwd(a)R, w) = fwd(a) w; the raw
     // lazy output (< (4+2L)q <= R) times a canonical w is a valid
     // Montgomery pair.
-    fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A);
-    if (!valid) return;
     const uint64_t *wp = wv + poly * G::N;
     uint64_t *dst = out + poly * G::N;
+#if FHE_FWDMUL_PREFETCH
+    if constexpr (G::P == 1) {
+        // w is loaded during the last pass (its HBM latency overlaps it)
+        uint64_t rw[G::E];
+        const uint32_t vo = LastIO<LOGN>::vo(tau);
+        auto hook = [&] {
+            const auto r = brsrc(wp);
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) rw[e] = bload(r, vo, LastIO<LOGN>::so(e));
+        };
+        fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A, 0, 0, hook);
+        W w[G::E];
+        coeffs_from_raw<G::E>(w, rw, A.q64, A.q64, A.mu64);
+        const auto ro = brsrc(dst);
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) bstore(ro, vo, LastIO<LOGN>::so(e), (uint64_t)A.ar.red1q(A.ar.mont(v[e], w[e])));
+        return;
+    }
+#endif
+    fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A);
+    if (!valid) return;
     // two chunks: 16 raw u64 w in flight at once would exceed 64 VGPRs
     constexpr int CH = G::E >= 8 ? G::E / 8 : G::E;
 #pragma unroll
     for (int c0 = 0; c0 < G::E; c0 += CH) {
         W w[CH];
-        load_coeffs<CH>(w, A.q64, A.q64, A.mu64, [&](int e) -> uint64_t {
-            return __builtin_nontemporal_load(wp + gidx<LOGN, G::NP - 1>(tau, c0 + e));
-        });
+        if constexpr (G::P == 1) {
+            const auto rw = brsrc(wp), ro = brsrc(dst);
+            const uint32_t vo = LastIO<LOGN>::vo(tau);
+            load_coeffs<CH>(w, A.q64, A.q64, A.mu64,
+                            [&](int e) -> uint64_t { return bload(rw, vo, LastIO<LOGN>::so(c0 + e)); });
 #pragma unroll
-        for (int e = 0; e < CH; ++e) {
-            const W x = A.ar.red1q(A.ar.mont(v[c0 + e], w[e]));
-            __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, c0 + e));
+            for (int e = 0; e < CH; ++e)
+                bstore(ro, vo, LastIO<LOGN>::so(c0 + e), (uint64_t)A.ar.red1q(A.ar.mont(v[c0 + e], w[e])));
+        } else {
+            load_coeffs<CH>(w, A.q64, A.q64, A.mu64, [&](int e) -> uint64_t {
+                return __builtin_nontemporal_load(wp + gidx<LOGN, G::NP - 1>(tau, c0 + e));
+            });
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                const W x = A.ar.red1q(A.ar.mont(v[c0 + e], w[e]));
+                __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, c0 + e));
+            }
         }
     }
 }

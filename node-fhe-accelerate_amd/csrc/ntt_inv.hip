@@ -17,13 +17,20 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
+    if (G::P == 1 && !valid) return;
     W v[G::E];
     const uint64_t *src = in + poly * G::N;
     const uint64_t lim = (uint64_t)A.ar.q2;  // GS inputs must be < 2q
+    if constexpr (G::P == 1) {
+        const auto r = brsrc(src);
+        const uint32_t vo = LastIO<LOGN>::vo(tau);
+        load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int e) -> uint64_t { return bload(r, vo, LastIO<LOGN>::so(e)); });
+    } else {
 #pragma unroll
-    for (int e = 0; e < G::E; ++e) {
-        uint64_t x = valid ? __builtin_nontemporal_load(src + gidx<LOGN, G::NP - 1>(tau, e)) : 0;
-        v[e] = load_lazy<W>(x, lim, A.q64, A.mu64);
+        for (int e = 0; e < G::E; ++e) {
+            uint64_t x = valid ? __builtin_nontemporal_load(src + gidx<LOGN, G::NP - 1>(tau, e)) : 0;
+            v[e] = load_lazy<W>(x, lim, A.q64, A.mu64);
+        }
     }
     inv_poly_from_regs<LOGN, NEGA>(lds, v, tau, out + poly * G::N, valid, A, A.ninv, A.untwist);
 }
@@ -33,19 +40,27 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 // full and the kernel is ALU-bound, so 16N extra bytes are cheap).  Keeping
 // both spectra in VGPRs cost 150-255 VGPRs (N <= 8192) or scratch spills
 // (N = 16384).
+#ifndef FHE_POLY_PREFETCH
+#define FHE_POLY_PREFETCH 1
+#endif
 #ifndef FHE_POLY_HBM_STASH
 #define FHE_POLY_HBM_STASH 0
+#endif
+#ifndef FHE_POLY_REG_STASH_14
+#define FHE_POLY_REG_STASH_14 0
 #endif
 template <int LOGN, typename W>
 constexpr int polymul_stash() {
     using G = Geo<LOGN>;
     if (LOGN < 5) return 0;
+    if (FHE_POLY_REG_STASH_14 && LOGN == 14 && sizeof(W) == 4) return 0;
     if (FHE_POLY_HBM_STASH && LOGN == 14) return 2;
     return G::P * (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024 ? 1 : 2;
 }
 template <int LOGN, typename W>
 constexpr int polymul_occ() {
     // with the stash in HBM the LDS footprint admits a second workgroup
+    if (polymul_stash<LOGN, W>() == 0 && LOGN >= 12) return Geo<LOGN>::template occ_waves<W>();
     return polymul_stash<LOGN, W>() == 2 && FHE_POLY_HBM_STASH ? Geo<LOGN>::template occ_waves<W>() : 1;
 }
 
@@ -62,9 +77,18 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     W *lds = lds_all + pl * G::LW;
     W *st = lds_all + G::P * G::LW + pl * G::N;
     uint64_t *crow = c + poly * G::N;
+    if (G::P == 1 && !valid) return;
     W v[G::E];
     W va[STASH == 0 ? G::E : 1];
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, a + poly * G::N, valid, A);
+    // P == 1: b's coefficients are loaded during fwd(a)'s last pass, so
+    // their HBM latency overlaps it (one workgroup per CU has no other
+    // workgroup to hide it behind).
+    constexpr bool PRE = G::P == 1 && FHE_POLY_PREFETCH && STASH != 0;
+    uint64_t rb[PRE ? G::E : 1];
+    auto hook = [&] {
+        if constexpr (PRE) load_raw<LOGN>(*reinterpret_cast<uint64_t(*)[G::E]>(rb), tau, b + poly * G::N);
+    };
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, a + poly * G::N, valid, A, 0, 0, hook);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const W x = fwd_to_canon<LAZY>(v[e], A);  // canonical: times a raw output below
@@ -79,7 +103,11 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     // u32 the reuse is cheaper than recomputing (measured, r05 A/B).
     uint32_t tb = tau;
     if constexpr (sizeof(W) == 8) asm volatile("" : "+v"(tb));
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A);
+    if constexpr (PRE)
+        fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A, 0, 0, NoHook{},
+                                               reinterpret_cast<uint64_t(*)[G::E]>(rb));
+    else
+        fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tb, e);
