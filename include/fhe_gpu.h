@@ -143,6 +143,54 @@ int fhe_external_product_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint
 int fhe_decompose_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const uint64_t *poly, uint64_t *out,
                         size_t npoly, int where);
 
+/* ---- BFV-style ciphertext multiplication (encryption.cpp:737-980) -------
+ * A ciphertext is its component polynomials, contiguous: ct [batch][2][n]
+ * (c0, c1); a degree-2 product [batch][3][n] (c0, c1, c2).
+ * fhe_ct_multiply_batch  EncryptionEngine::multiply (:737-798): is_ntt = 0
+ *   for coefficient-form inputs (4 forward + 3 inverse transforms in one
+ *   kernel), 1 when both inputs are already NTT-domain (tensor only).
+ * fhe_relin_key_prepare  the KeySwitchKey pairs (a_l, b_l) of
+ *   key_manager.cpp:296-324, rlk [level][2][n], into the NTT-domain form
+ *   fhe_relinearize_batch consumes (same shape).
+ * fhe_relinearize_batch  EncryptionEngine::relinearize (:904-980): digit l
+ *   of c2 is (c2 >> l*base_log) & (2^base_log - 1); out [batch][2][n] =
+ *   (c0 + sum_l d_l * b_l, c1 + sum_l d_l * a_l).  level = number of key
+ *   pairs used (the reference's min(decomp_level, keys.size())); level 0
+ *   copies c0, c1.  Requires (level - 1) * base_log < 64, 1 <= base_log <= 63.
+ * fhe_ct_multiply_relin_batch  multiply_relin (:800-807): both steps. */
+int fhe_ct_multiply_batch(fhe_ctx *ctx, const uint64_t *ct1, const uint64_t *ct2, uint64_t *out, size_t batch,
+                          int is_ntt, int where);
+int fhe_relin_key_prepare(fhe_ctx *ctx, uint32_t level, const uint64_t *rlk, uint64_t *rlk_ntt, int where);
+int fhe_relinearize_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const uint64_t *ct3,
+                          const uint64_t *rlk_ntt, uint64_t *out, size_t batch, int where);
+int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const uint64_t *ct1,
+                                const uint64_t *ct2, const uint64_t *rlk_ntt, uint64_t *out, size_t batch,
+                                int where);
+
+/* ---- TFHE bootstrapping pieces (bootstrap_engine.cpp) --------------------
+ * GLWE [batch][k+1][n] as above; LWE masks [batch][dim], bodies [batch].
+ * fhe_glwe_rotate_batch    multiply_glwe_by_monomial (:249-261) by X^rot[c].
+ * fhe_cmux_batch           cmux (:520-540): ct0 + ggsw (x) (ct1 - ct0).
+ * fhe_blind_rotate_batch   blind_rotate (:547-577) of acc in place, for each
+ *   ciphertext c with its own LWE (lwe_a[c], lwe_b[c]) modulo lwe_q; bsk_ntt
+ *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).
+ * fhe_sample_extract_batch sample_extract (:594-624): lwe_a [batch][k*n].
+ * fhe_key_switch_batch     key_switch (:630-677): ksk_a [in_dim*level][out_dim]
+ *   (the `first` polynomials of ksk.keys, entry i*level + l), ksk_b
+ *   [in_dim*level] (coefficient 0 of each `second` polynomial). */
+int fhe_glwe_rotate_batch(fhe_ctx *ctx, uint32_t k, const int32_t *rot, const uint64_t *glwe, uint64_t *out,
+                          size_t batch, int where);
+int fhe_cmux_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *ggsw_ntt,
+                   const uint64_t *ct0, const uint64_t *ct1, uint64_t *out, size_t batch, int where);
+int fhe_blind_rotate_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
+                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint64_t lwe_q, const uint64_t *bsk_ntt,
+                           uint64_t *acc, size_t batch, int where);
+int fhe_sample_extract_batch(fhe_ctx *ctx, uint32_t k, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
+                             size_t batch, int where);
+int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t in_dim, uint32_t out_dim,
+                         const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a, const uint64_t *lwe_b,
+                         uint64_t *out_a, uint64_t *out_b, size_t batch, int where, int device, void *hip_stream);
+
 /* ---- context-free modular kernels --------------------------------------- */
 /* BarrettReducer::barrett_mul contract (modular_arithmetic.cpp:268-280):
  * c[i] = a[i]*b[i] mod q for any u64 inputs, any q != 0. stream may be NULL. */

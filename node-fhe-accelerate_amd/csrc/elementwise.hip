@@ -220,6 +220,33 @@ k_decompose(const uint64_t *__restrict__ poly, uint64_t *__restrict__ out, uint3
     }
 }
 
+// EncryptionEngine::multiply for NTT-form ciphertexts (encryption.cpp:
+// 762-780 without the transforms): c0 = x0 y0, c1 = x0 y1 + x1 y0, c2 = x1 y1
+// with pointwise_multiply's exact (a*b) % q and mod_add.
+__global__ void __launch_bounds__(kBlock)
+k_tensor_ntt(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *__restrict__ out,
+             uint32_t n, size_t batch, ModConsts m) {
+    const size_t total = (size_t)n * batch;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t b = i / n, k = i % n;
+        const uint64_t x0 = x[(2 * b) * n + k], x1 = x[(2 * b + 1) * n + k];
+        const uint64_t y0 = y[(2 * b) * n + k], y1 = y[(2 * b + 1) * n + k];
+        const uint64_t c0 = modmul1(x0, y0, m), c2 = modmul1(x1, y1, m);
+        const uint64_t c1 = addsub1(modmul1(x0, y1, m), modmul1(x1, y0, m), 0, m);
+        out[(3 * b) * n + k] = c0;
+        out[(3 * b + 1) * n + k] = c1;
+        out[(3 * b + 2) * n + k] = c2;
+    }
+}
+
+hipError_t launch_tensor_ntt(const ModConsts &m, const uint64_t *x, const uint64_t *y, uint64_t *out, uint32_t n,
+                             size_t batch, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tensor_ntt, dim3(grid_for((size_t)n * batch)), dim3(kBlock), 0, s, x, y, out, n, batch, m);
+    return hipGetLastError();
+}
+
 hipError_t launch_modmul(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
                          hipStream_t s) {
     if (n == 0) return hipSuccess;

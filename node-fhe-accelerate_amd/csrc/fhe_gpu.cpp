@@ -264,6 +264,113 @@ int run_poly_op(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, size_t batch, 
     return staged(c, ins, b ? 2 : 1, in_per, out, out_per, batch, fn);
 }
 
+// ---------------------------------------------------------------- ciphertext ops
+// Host-resident calls of the multi-buffer entry points: every host buffer is
+// copied to a device temporary (inputs) or allocated (outputs), the device
+// path runs, outputs are copied back.  No chunking: these ops are used at
+// ciphertext-batch sizes far below HBM capacity.
+class HostStage {
+    std::vector<void *> allocs_;
+    struct Back { void *host; const void *dev; size_t bytes; };
+    std::vector<Back> back_;
+    hipStream_t s_;
+
+  public:
+    explicit HostStage(hipStream_t s) : s_(s) {}
+    ~HostStage() {
+        for (void *p : allocs_) (void)hipFree(p);
+    }
+    // where == FHE_DEVICE: pass through; else stage.  dir: 1 in, 2 out, 3 in/out.
+    template <typename T>
+    int map(int where, T *&ptr, size_t bytes, int dir) {
+        if (where == FHE_DEVICE || ptr == nullptr || bytes == 0) return FHE_OK;
+        void *d = nullptr;
+        hipError_t e = hipMalloc(&d, bytes);
+        if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMalloc: out of memory");
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(stage)");
+        allocs_.push_back(d);
+        if (dir & 1) HIP_TRY(hipMemcpyAsync(d, (const void *)ptr, bytes, hipMemcpyHostToDevice, s_), "hipMemcpy(H2D)");
+        if (dir & 2) back_.push_back({(void *)ptr, d, bytes});
+        ptr = (T *)d;
+        return FHE_OK;
+    }
+    int finish() {
+        for (auto &b : back_) HIP_TRY(hipMemcpyAsync(b.host, b.dev, b.bytes, hipMemcpyDeviceToHost, s_), "hipMemcpy(D2H)");
+        HIP_TRY(hipStreamSynchronize(s_), "hipStreamSynchronize");
+        return FHE_OK;
+    }
+};
+#define FHE_TRY(expr)                 \
+    do {                              \
+        if (int _rc = (expr)) return _rc; \
+    } while (0)
+
+static bool overlaps(const void *a, size_t an, const void *b, size_t bn) {
+    const char *x = (const char *)a, *y = (const char *)b;
+    return a && b && an && bn && x < y + bn && y < x + an;
+}
+
+static int check_common(const fhe_ctx *c, int where, size_t batch) {
+    if (int rc = check_ctx(c)) return rc;
+    if (where != FHE_HOST && where != FHE_DEVICE) return fail(FHE_ERR_INVALID_ARG, "where must be FHE_HOST or FHE_DEVICE");
+    (void)batch;
+    return FHE_OK;
+}
+static int check_fused(const fhe_ctx *c, const char *what) {
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN)
+        return fail(FHE_ERR_UNSUPPORTED, std::string(what) + " implemented for degrees up to 16384");
+    return FHE_OK;
+}
+static int check_relin_decomp(uint32_t base_log, uint32_t level) {
+    if (base_log == 0 || base_log > 63 || (level > 0 && (u64)(level - 1) * base_log >= 64))
+        return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    return FHE_OK;
+}
+
+// Composed (unfused) ciphertext multiply for n > 16384: 4 forward
+// transforms, tensor, 3 inverse transforms through a temporary.
+static int ct_mul_composed(fhe_ctx *c, const u64 *x, const u64 *y, u64 *out, size_t batch) {
+    const size_t n = c->n;
+    void *t = nullptr;
+    HIP_TRY(hipMalloc(&t, batch * 4 * n * 8), "hipMalloc(ct_mul)");
+    u64 *tx = (u64 *)t, *ty = tx + batch * 2 * n;
+    hipError_t e = FHE_NS::launch_fwd(c->plan, x, tx, batch * 2, 0);
+    if (e == hipSuccess) e = FHE_NS::launch_fwd(c->plan, y, ty, batch * 2, 0);
+    if (e == hipSuccess) e = FHE_NS::launch_tensor_ntt(mod_consts(c->q), tx, ty, out, c->n, batch, c->stream);
+    if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, out, out, batch * 3);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(t);
+    if (e != hipSuccess) return hip_fail(e, "ct_multiply");
+    return FHE_OK;
+}
+
+static int ct_mul_device(fhe_ctx *c, const u64 *x, const u64 *y, u64 *out, size_t batch, int is_ntt) {
+    const size_t in_b = batch * 2 * c->n * 8, out_b = batch * 3 * c->n * 8;
+    if (overlaps(out, out_b, x, in_b) || overlaps(out, out_b, y, in_b))
+        return fail(FHE_ERR_INVALID_ARG, "output must not overlap the input ciphertexts");
+    if (is_ntt) {
+        HIP_TRY(FHE_NS::launch_tensor_ntt(mod_consts(c->q), x, y, out, c->n, batch, c->stream), "tensor kernel");
+        return FHE_OK;
+    }
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN) return ct_mul_composed(c, x, y, out, batch);
+    HIP_TRY(FHE_NS::launch_ct_mul(c->plan, x, y, out, batch), "ct_mul kernel");
+    return FHE_OK;
+}
+
+static int relin_device(fhe_ctx *c, uint32_t base_log, uint32_t level, const u64 *ct3, const u64 *rlk, u64 *out,
+                        size_t batch) {
+    const size_t n = c->n;
+    if (overlaps(out, batch * 2 * n * 8, ct3, batch * 3 * n * 8))
+        return fail(FHE_ERR_INVALID_ARG, "output must not overlap the input ciphertexts");
+    if (level == 0) {  // no key pairs: c0, c1 copied (encryption.cpp:966-972)
+        HIP_TRY(hipMemcpy2DAsync(out, 2 * n * 8, ct3, 3 * n * 8, 2 * n * 8, batch, hipMemcpyDeviceToDevice, c->stream),
+                "hipMemcpy2D");
+        return FHE_OK;
+    }
+    HIP_TRY(FHE_NS::launch_relin(c->plan, (int)level, (int)base_log, ct3, rlk, out, batch), "relin kernel");
+    return FHE_OK;
+}
+
 }  // namespace
 
 // =====================================================================
@@ -519,6 +626,204 @@ int fhe_decompose_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uin
                        [&](const u64 *const *d, u64 *o, size_t nb) {
                            return FHE_NS::launch_decompose(m, d[0], o, c->n, nb, base_log, level, c->stream);
                        });
+}
+
+
+int fhe_ct_multiply_batch(fhe_ctx *c, const uint64_t *ct1, const uint64_t *ct2, uint64_t *out, size_t batch,
+                          int is_ntt, int where) {
+    FHE_TRY(check_common(c, where, batch));
+    if (batch == 0) return FHE_OK;
+    if (!ct1 || !ct2 || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, ct1, batch * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, ct2, batch * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, out, batch * 3 * n * 8, 2));
+    FHE_TRY(ct_mul_device(c, ct1, ct2, out, batch, is_ntt));
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_relin_key_prepare(fhe_ctx *c, uint32_t level, const uint64_t *rlk, uint64_t *rlk_ntt, int where) {
+    if (int rc = check_ctx(c)) return rc;
+    FHE_TRY(check_fused(c, "relinearisation"));
+    return run_poly_op(c, rlk, nullptr, rlk_ntt, (size_t)2 * level, where, c->n, c->n,
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 1); });
+}
+
+int fhe_relinearize_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *ct3,
+                          const uint64_t *rlk_ntt, uint64_t *out, size_t batch, int where) {
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_fused(c, "relinearisation"));
+    FHE_TRY(check_relin_decomp(base_log, level));
+    if (batch == 0) return FHE_OK;
+    if (!ct3 || !out || (level && !rlk_ntt)) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, ct3, batch * 3 * n * 8, 1));
+    FHE_TRY(hs.map(where, rlk_ntt, (size_t)level * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, out, batch * 2 * n * 8, 2));
+    FHE_TRY(relin_device(c, base_log, level, ct3, rlk_ntt, out, batch));
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_ct_multiply_relin_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *ct1,
+                                const uint64_t *ct2, const uint64_t *rlk_ntt, uint64_t *out, size_t batch,
+                                int where) {
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_fused(c, "relinearisation"));
+    FHE_TRY(check_relin_decomp(base_log, level));
+    if (batch == 0) return FHE_OK;
+    if (!ct1 || !ct2 || !out || (level && !rlk_ntt)) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, ct1, batch * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, ct2, batch * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, rlk_ntt, (size_t)level * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, out, batch * 2 * n * 8, 2));
+    u64 *ct3 = nullptr;
+    HIP_TRY(hipMalloc((void **)&ct3, batch * 3 * n * 8), "hipMalloc(ct3)");
+    int rc = ct_mul_device(c, ct1, ct2, ct3, batch, 0);
+    if (rc == FHE_OK) rc = relin_device(c, base_log, level, ct3, rlk_ntt, out, batch);
+    if (rc == FHE_OK && where == FHE_HOST) rc = hs.finish();
+    if (rc == FHE_OK && where == FHE_DEVICE) {
+        hipError_t e = hipStreamSynchronize(c->stream);  // ct3 is freed below
+        if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    }
+    (void)hipFree(ct3);
+    return rc;
+}
+
+static int check_tfhe(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level) {
+    FHE_TRY(check_fused(c, "external product"));
+    if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
+    if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
+        return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    return FHE_OK;
+}
+
+int fhe_glwe_rotate_batch(fhe_ctx *c, uint32_t k, const int32_t *rot, const uint64_t *glwe, uint64_t *out,
+                          size_t batch, int where) {
+    FHE_TRY(check_common(c, where, batch));
+    if (batch == 0) return FHE_OK;
+    if (!rot || !glwe || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const size_t bytes = batch * (k + 1) * c->n * 8;
+    DeviceGuard g(c->device);
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, rot, batch * sizeof(int32_t), 1));
+    FHE_TRY(hs.map(where, glwe, bytes, 1));
+    FHE_TRY(hs.map(where, out, bytes, 2));
+    if (overlaps(glwe, bytes, out, bytes)) return fail(FHE_ERR_INVALID_ARG, "output must not overlap the input");
+    HIP_TRY(FHE_NS::launch_rotate(mod_consts(c->q), glwe, out, c->n, k + 1, batch, rot, nullptr, 0, c->stream),
+            "rotate kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *ggsw_ntt,
+                   const uint64_t *ct0, const uint64_t *ct1, uint64_t *out, size_t batch, int where) {
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_tfhe(c, k, base_log, level));
+    if (batch == 0) return FHE_OK;
+    if (!ggsw_ntt || !ct0 || !ct1 || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const size_t n = c->n, bytes = batch * (k + 1) * n * 8;
+    DeviceGuard g(c->device);
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, ggsw_ntt, (size_t)(k + 1) * level * (k + 1) * n * 8, 1));
+    FHE_TRY(hs.map(where, ct0, bytes, 1));
+    FHE_TRY(hs.map(where, ct1, bytes, 1));
+    FHE_TRY(hs.map(where, out, bytes, 2));
+    if (overlaps(out, bytes, ct0, bytes) || overlaps(out, bytes, ct1, bytes))
+        return fail(FHE_ERR_INVALID_ARG, "output must not overlap the inputs");
+    HIP_TRY(FHE_NS::launch_cmux(c->plan, (int)k + 1, (int)level, (int)base_log, ggsw_ntt, ct0, ct1, out, batch),
+            "cmux kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
+                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint64_t lwe_q, const uint64_t *bsk_ntt,
+                           uint64_t *acc, size_t batch, int where) {
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_tfhe(c, k, base_log, level));
+    if (lwe_q == 0) return fail(FHE_ERR_ZERO_MODULUS, "LWE modulus must be non-zero");
+    if (batch == 0) return FHE_OK;
+    if (!lwe_b || !acc || (lwe_dim && (!lwe_a || !bsk_ntt))) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const size_t n = c->n, bytes = batch * (k + 1) * n * 8;
+    const size_t ggsw_words = (size_t)(k + 1) * level * (k + 1) * n;
+    DeviceGuard g(c->device);
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, lwe_a, batch * lwe_dim * 8, 1));
+    FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
+    FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
+    FHE_TRY(hs.map(where, acc, bytes, 3));
+    u64 *tmp = nullptr;
+    HIP_TRY(hipMalloc((void **)&tmp, bytes), "hipMalloc(blind rotate)");
+    // acc <- X^-round(b 2N / q) acc, into tmp; then lwe_dim CMux steps
+    // ping-ponging tmp <-> acc; the result is copied back into acc if the
+    // step count is even (it ended in tmp).
+    hipError_t e = FHE_NS::launch_rotate(mod_consts(c->q), acc, tmp, c->n, k + 1, batch, nullptr, lwe_b, lwe_q, c->stream);
+    u64 *cur = tmp, *nxt = acc;
+    for (uint32_t i = 0; e == hipSuccess && i < lwe_dim; ++i) {
+        e = FHE_NS::launch_cmux_rotate(c->plan, (int)k + 1, (int)level, (int)base_log, cur, bsk_ntt + ggsw_words * i, nxt,
+                                       batch, lwe_a, lwe_dim, i, lwe_q);
+        std::swap(cur, nxt);
+    }
+    if (e == hipSuccess && cur != acc) e = hipMemcpyAsync(acc, cur, bytes, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return hip_fail(e, "blind rotate");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_sample_extract_batch(fhe_ctx *c, uint32_t k, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
+                             size_t batch, int where) {
+    FHE_TRY(check_common(c, where, batch));
+    if (batch == 0) return FHE_OK;
+    if (!glwe || !lwe_b || (k && !lwe_a)) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    const size_t n = c->n;
+    DeviceGuard g(c->device);
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, glwe, batch * (k + 1) * n * 8, 1));
+    FHE_TRY(hs.map(where, lwe_a, batch * k * n * 8, 2));
+    FHE_TRY(hs.map(where, lwe_b, batch * 8, 2));
+    if (k == 0) {  // body only
+        HIP_TRY(hipMemcpy2DAsync(lwe_b, 8, glwe, n * 8, 8, batch, hipMemcpyDeviceToDevice, c->stream), "hipMemcpy2D");
+    } else {
+        HIP_TRY(FHE_NS::launch_sample_extract(mod_consts(c->q), glwe, lwe_a, lwe_b, c->n, k, batch, c->stream),
+                "sample extract kernel");
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t in_dim, uint32_t out_dim,
+                         const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a, const uint64_t *lwe_b,
+                         uint64_t *out_a, uint64_t *out_b, size_t batch, int where, int device, void *stream) {
+    if (q < 2) return fail(FHE_ERR_ZERO_MODULUS, "key switch modulus must be >= 2");
+    if (where != FHE_HOST && where != FHE_DEVICE) return fail(FHE_ERR_INVALID_ARG, "where must be FHE_HOST or FHE_DEVICE");
+    if (base_log == 0 || base_log > 63 || (level > 0 && (u64)(level - 1) * base_log >= 64))
+        return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    if (batch == 0) return FHE_OK;
+    const size_t entries = (size_t)in_dim * level;
+    if (!lwe_b || !out_b || (entries && (!lwe_a || !ksk_b)) || (entries && out_dim && !ksk_a) || (out_dim && !out_a))
+        return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(FHE_ERR_DEVICE, "no HIP device available (the backend has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(FHE_ERR_INVALID_ARG, "device ordinal out of range");
+    DeviceGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    HostStage hs(s);
+    FHE_TRY(hs.map(where, ksk_a, entries * out_dim * 8, 1));
+    FHE_TRY(hs.map(where, ksk_b, entries * 8, 1));
+    FHE_TRY(hs.map(where, lwe_a, batch * in_dim * 8, 1));
+    FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
+    FHE_TRY(hs.map(where, out_a, batch * out_dim * 8, 2));
+    FHE_TRY(hs.map(where, out_b, batch * 8, 2));
+    HIP_TRY(FHE_NS::launch_key_switch(mod_consts(q), base_log, level, in_dim, out_dim, ksk_a, ksk_b, lwe_a, lwe_b, out_a,
+                                      out_b, batch, s),
+            "key switch kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 
 // ---------------------------------------------------------------- context-free kernels

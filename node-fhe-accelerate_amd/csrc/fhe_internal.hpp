@@ -40,6 +40,21 @@ hipError_t launch_big(const Plan &p, int op, const uint64_t *a, const uint64_t *
 hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const uint64_t *glwe,
                           const uint64_t *ggsw, uint64_t *out, size_t batch);
 
+// Relinearisation (EncryptionEngine::relinearize): ct3 [batch][3][n],
+// rlk [level][2][n] (a_l, b_l) in NTT-Montgomery form -> out [batch][2][n].
+hipError_t launch_relin(const Plan &p, int level, int base_log, const uint64_t *ct3, const uint64_t *rlk,
+                        uint64_t *out, size_t batch);
+// One blind-rotation CMux step over a batch of GLWE accumulators (ping-pong
+// buffers acc_in -> acc_out); step = LWE mask index i, bsk[i] = ggsw.
+hipError_t launch_cmux_rotate(const Plan &p, int k1, int level, int base_log, const uint64_t *acc_in,
+                              const uint64_t *ggsw, uint64_t *acc_out, size_t batch, const uint64_t *lwe_a,
+                              uint32_t lwe_dim, uint32_t step, uint64_t lwe_q);
+// CMux(ggsw, ct0, ct1) = ct0 + ggsw (x) (ct1 - ct0)
+hipError_t launch_cmux(const Plan &p, int k1, int level, int base_log, const uint64_t *ggsw, const uint64_t *ct0,
+                       const uint64_t *ct1, uint64_t *out, size_t batch);
+// Ciphertext multiply (coefficient form): x, y [batch][2][n] -> out [batch][3][n]
+hipError_t launch_ct_mul(const Plan &p, const uint64_t *x, const uint64_t *y, uint64_t *out, size_t batch);
+
 // Elementwise kernels (elementwise.hip).
 struct ModConsts {
     uint64_t q, mu, qinv, r2;  // mu = floor(2^64/q); Montgomery R = 2^64
@@ -54,6 +69,21 @@ hipError_t launch_mul_scalar(const ModConsts &m, const uint64_t *a, uint64_t sc,
                              size_t n, hipStream_t s);
 hipError_t launch_ml_montmul(const uint64_t consts[7], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
                              hipStream_t s);
+// Tensor product of NTT-form ciphertexts: x, y [batch][2][n] -> [batch][3][n]
+hipError_t launch_tensor_ntt(const ModConsts &m, const uint64_t *x, const uint64_t *y, uint64_t *out, uint32_t n,
+                             size_t batch, hipStream_t s);
+// GLWE rotation by X^r (multiply_glwe_by_monomial): polys per ciphertext =
+// k1; r = rot[c], or when rot == nullptr r = -(int32)((b[c]*2N + q/2)/q)
+// (blind_rotate's initial rotation by the LWE body).
+hipError_t launch_rotate(const ModConsts &m, const uint64_t *in, uint64_t *out, uint32_t n, uint32_t k1, size_t batch,
+                         const int32_t *rot, const uint64_t *lwe_b, uint64_t lwe_q, hipStream_t s);
+// sample_extract: glwe [batch][k+1][n] -> lwe_a [batch][k*n], lwe_b [batch]
+hipError_t launch_sample_extract(const ModConsts &m, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
+                                 uint32_t n, uint32_t k, size_t batch, hipStream_t s);
+// LWE key switch (BootstrapEngine::key_switch)
+hipError_t launch_key_switch(const ModConsts &m, uint32_t base_log, uint32_t level, uint32_t in_dim, uint32_t out_dim,
+                             const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a,
+                             const uint64_t *lwe_b, uint64_t *out_a, uint64_t *out_b, size_t batch, hipStream_t s);
 hipError_t launch_decompose(const ModConsts &m, const uint64_t *poly, uint64_t *out, uint32_t n, size_t npoly,
                             uint32_t base_log, uint32_t level, hipStream_t s);
 

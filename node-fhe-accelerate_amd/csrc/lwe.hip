@@ -1,0 +1,183 @@
+// lwe.hip -- the non-transform pieces of TFHE bootstrapping, batched over
+// ciphertexts:
+//
+//   rotate         multiply_glwe_by_monomial / rotate_polynomial
+//                  (bootstrap_engine.cpp:249-261, 122-145); also blind_rotate's
+//                  initial rotation by -round(b * 2N / q) (:555-557)
+//   sample_extract (:594-624)
+//   key_switch     (:630-677): out_a = -sum_{i,l} d_il * ksk_a[i,l]  (mod q),
+//                  out_b = b - sum_{i,l} d_il * ksk_b[i,l][0], with the
+//                  reference's u64-wrapping digit * key products, its `digit
+//                  == 0` skip and its raw (unreduced) body when every digit
+//                  is zero.
+//
+// rotate / sample_extract are HBM gathers.  key_switch is a modular
+// matrix-vector product per ciphertext over a key shared by the batch: a
+// workgroup takes 256 output coefficients of CT ciphertexts, stages their
+// digits in LDS chunk by chunk and streams the key rows (coalesced along the
+// output index) once per CT ciphertexts.
+#include "fhe_internal.hpp"
+#include "lwe_ops.hpp"
+
+namespace FHE_NS {
+
+static constexpr int kLweBlock = 256;
+
+static inline size_t lwe_grid(size_t work) {
+    size_t g = (work + kLweBlock - 1) / kLweBlock;
+    const size_t cap = 256 * 16;
+    return g < 1 ? 1 : (g > cap ? cap : g);
+}
+
+__global__ void __launch_bounds__(kLweBlock)
+k_rotate(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint32_t n, uint32_t k1, size_t batch,
+         const int32_t *__restrict__ rot, const uint64_t *__restrict__ lwe_b, uint64_t lwe_q, uint64_t q,
+         uint64_t mu) {
+    const size_t total = (size_t)batch * k1 * n;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t poly = i / n, c = poly / k1;
+        const uint32_t p = (uint32_t)(i % n);
+        const int32_t r = rot ? rot[c] : -rot_amount(lwe_b[c], n, lwe_q);
+        out[i] = rotated_at(in + poly * n, p, rot_norm(r, n), n, q, mu);
+    }
+}
+
+__global__ void __launch_bounds__(kLweBlock)
+k_sample_extract(const uint64_t *__restrict__ glwe, uint64_t *__restrict__ lwe_a, uint64_t *__restrict__ lwe_b,
+                 uint32_t n, uint32_t k, size_t batch, uint64_t q, uint64_t mu) {
+    const size_t per = (size_t)k * n, total = batch * per;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
+        const size_t c = x / per;
+        const uint32_t i = (uint32_t)((x % per) / n), j = (uint32_t)(x % n);
+        const uint64_t *mask = glwe + (c * (k + 1) + i) * n;
+        lwe_a[x] = j == 0 ? mask[0] : red_q(q - mask[n - j], q, mu);
+        if (i == 0 && j == 0) lwe_b[c] = glwe[(c * (k + 1) + k) * n];
+    }
+}
+
+// ((d * key) mod 2^64) % q  -- key_switch's `(digit * ksk_entry.first[j]) % q`
+__device__ __forceinline__ uint64_t ks_term(uint64_t d, uint64_t key, uint64_t q, uint64_t mu) {
+    return mod64_slow(d * key, q, mu);
+}
+
+constexpr int kKsCt = 16;     // ciphertexts per workgroup (key rows read once per 16)
+constexpr int kKsChunk = 256; // (i, l) entries staged per LDS round
+
+__global__ void __launch_bounds__(kLweBlock)
+k_key_switch_a(const uint64_t *__restrict__ ksk_a, const uint64_t *__restrict__ lwe_a, uint64_t *__restrict__ out_a,
+               uint32_t in_dim, uint32_t out_dim, uint32_t level, uint32_t base_log, size_t batch, uint64_t q,
+               uint64_t mu) {
+    __shared__ uint64_t dig[kKsChunk][kKsCt];
+    const uint32_t j = blockIdx.x * kLweBlock + threadIdx.x;
+    const size_t c0 = (size_t)blockIdx.y * kKsCt;
+    const uint64_t mask = (1ull << base_log) - 1;
+    const uint32_t entries = in_dim * level;
+    uint64_t acc[kKsCt];
+#pragma unroll
+    for (int c = 0; c < kKsCt; ++c) acc[c] = 0;
+    for (uint32_t e0 = 0; e0 < entries; e0 += kKsChunk) {
+        const uint32_t ne = entries - e0 < (uint32_t)kKsChunk ? entries - e0 : (uint32_t)kKsChunk;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < ne * kKsCt; t += kLweBlock) {
+            const uint32_t e = t / kKsCt, c = t % kKsCt;
+            const uint32_t idx = e0 + e, i = idx / level, l = idx % level;
+            const uint32_t shift = (level - 1 - l) * base_log;
+            dig[e][c] = c0 + c < batch ? (lwe_a[(c0 + c) * in_dim + i] >> shift) & mask : 0;
+        }
+        __syncthreads();
+        if (j < out_dim) {
+            const uint64_t *krow = ksk_a + (size_t)e0 * out_dim + j;
+            for (uint32_t e = 0; e < ne; ++e) {
+                const uint64_t key = krow[(size_t)e * out_dim];
+#pragma unroll
+                for (int c = 0; c < kKsCt; ++c) {
+                    const uint64_t d = dig[e][c];
+                    if (d == 0) continue;  // uniform across the workgroup
+                    acc[c] = addq(acc[c], ks_term(d, key, q, mu), q);
+                }
+            }
+        }
+    }
+    if (j < out_dim) {
+#pragma unroll
+        for (int c = 0; c < kKsCt; ++c)
+            if (c0 + c < batch) out_a[(c0 + c) * out_dim + j] = acc[c] == 0 ? 0 : q - acc[c];
+    }
+}
+
+// One wavefront per ciphertext: sum of the body terms and the first
+// non-zero digit (whose update also reduces the raw body).
+__global__ void __launch_bounds__(64)
+k_key_switch_b(const uint64_t *__restrict__ ksk_b, const uint64_t *__restrict__ lwe_a,
+               const uint64_t *__restrict__ lwe_b, uint64_t *__restrict__ out_b, uint32_t in_dim, uint32_t level,
+               uint32_t base_log, uint64_t q, uint64_t mu) {
+    const size_t c = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t mask = (1ull << base_log) - 1;
+    const uint32_t entries = in_dim * level;
+    uint64_t s = 0;
+    uint32_t first = 0xFFFFFFFFu;
+    for (uint32_t idx = lane; idx < entries; idx += 64) {
+        const uint32_t i = idx / level, l = idx % level;
+        const uint64_t d = (lwe_a[c * in_dim + i] >> ((level - 1 - l) * base_log)) & mask;
+        if (d == 0) continue;
+        s = addq(s, ks_term(d, ksk_b[idx], q, mu), q);
+        first = first < idx ? first : idx;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t so = __shfl_xor(s, off, 64);
+        const uint32_t fo = __shfl_xor(first, off, 64);
+        s = addq(s, so, q);
+        first = first < fo ? first : fo;
+    }
+    if (lane == 0) {
+        const uint64_t b = lwe_b[c];
+        if (first == 0xFFFFFFFFu) {
+            out_b[c] = b;
+        } else {
+            const uint32_t i = first / level, l = first % level;
+            const uint64_t d = (lwe_a[c * in_dim + i] >> ((level - 1 - l) * base_log)) & mask;
+            const uint64_t t1 = ks_term(d, ksk_b[first], q, mu);
+            const uint64_t b1 = mod64_slow(b + q - t1, q, mu);  // u64 wrap as in the reference
+            out_b[c] = subq(b1, subq(s, t1, q), q);
+        }
+    }
+}
+
+hipError_t launch_rotate(const ModConsts &m, const uint64_t *in, uint64_t *out, uint32_t n, uint32_t k1, size_t batch,
+                         const int32_t *rot, const uint64_t *lwe_b, uint64_t lwe_q, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rotate, dim3(lwe_grid((size_t)batch * k1 * n)), dim3(kLweBlock), 0, s, in, out, n, k1, batch,
+                       rot, lwe_b, lwe_q, m.q, m.mu);
+    return hipGetLastError();
+}
+
+hipError_t launch_sample_extract(const ModConsts &m, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
+                                 uint32_t n, uint32_t k, size_t batch, hipStream_t s) {
+    if (batch == 0 || k == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sample_extract, dim3(lwe_grid((size_t)batch * k * n)), dim3(kLweBlock), 0, s, glwe, lwe_a,
+                       lwe_b, n, k, batch, m.q, m.mu);
+    return hipGetLastError();
+}
+
+hipError_t launch_key_switch(const ModConsts &m, uint32_t base_log, uint32_t level, uint32_t in_dim, uint32_t out_dim,
+                             const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a,
+                             const uint64_t *lwe_b, uint64_t *out_a, uint64_t *out_b, size_t batch, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    // grid.y <= 65535 workgroups of kKsCt ciphertexts per launch
+    const size_t per_launch = (size_t)65535 * kKsCt;
+    for (size_t b0 = 0; out_dim > 0 && b0 < batch; b0 += per_launch) {
+        const size_t nb = batch - b0 < per_launch ? batch - b0 : per_launch;
+        const dim3 grid((out_dim + kLweBlock - 1) / kLweBlock, (unsigned)((nb + kKsCt - 1) / kKsCt));
+        hipLaunchKernelGGL(k_key_switch_a, grid, dim3(kLweBlock), 0, s, ksk_a, lwe_a + b0 * in_dim,
+                           out_a + b0 * out_dim, in_dim, out_dim, level, base_log, nb, m.q, m.mu);
+        if (hipError_t e = hipGetLastError()) return e;
+    }
+    hipLaunchKernelGGL(k_key_switch_b, dim3((unsigned)batch), dim3(64), 0, s, ksk_b, lwe_a, lwe_b, out_b, in_dim, level,
+                       base_log, m.q, m.mu);
+    return hipGetLastError();
+}
+
+}  // namespace FHE_NS

@@ -1,0 +1,177 @@
+// ntt_cipher.hip -- ciphertext x ciphertext multiplication
+// (EncryptionEngine::multiply, encryption.cpp:737-798) for coefficient-form
+// ciphertexts, one kernel per batch:
+//
+//   X0 = fwd(ct1.c0)  X1 = fwd(ct1.c1)  Y0 = fwd(ct2.c0)  Y1 = fwd(ct2.c1)
+//   c0 = inv(X0 Y0)   c1 = inv(X0 Y1 + X1 Y0)   c2 = inv(X1 Y1)
+//
+// The reference runs 4 forward + 3 inverse transforms on cloned
+// polynomials, 4 pointwise products and an add, each a separate pass over
+// memory.  Here one workgroup owns one ciphertext pair and runs the 7
+// transforms back to back through registers and LDS; the inputs are read
+// once and the three outputs written once (56 B per coefficient).  Because
+// all products are exact over Z_q, inv(X0 Y1) + inv(X1 Y0) == inv(X0 Y1 +
+// X1 Y0) bit for bit.
+//
+// Between transforms a thread only touches its own positions (the last
+// forward pass layout), so three spectra are parked in "slots" without
+// synchronisation: LDS when it fits next to the exchange buffer, otherwise
+// rows 1 and 2 of this ciphertext's own output (overwritten last) and LDS or
+// registers for the third.  Schedule:
+//   1. fwd(x0)            -> A = X0
+//   2. fwd(y0)  = Y0      -> B = Y0,  c0 = inv(A Y0)               (row 0)
+//   3. fwd(x1)  = X1      -> C = X1 B (part of c1),  B = X1
+//   4. fwd(y1)  = Y1      -> c1 = C + A Y1,  C = B Y1 (= c2 spectrum)
+//                            inv(c1) -> row 1, inv(C) -> row 2
+// Products are Montgomery (x R^-1); the R is folded into the inverse's N^-1
+// (ninv_r), as in k_polymul.
+#include "fhe_internal.hpp"
+
+namespace FHE_NS {
+
+// Slots held in LDS: 3 (all), 1 (C only; A, B in HBM rows) or 0 (C in VGPRs).
+template <int LOGN, typename W>
+constexpr int ctmul_lds_slots() {
+    using G = Geo<LOGN>;
+    if (G::P * (G::LW + 3 * G::N) * (int)sizeof(W) <= 160 * 1024) return 3;
+    if (G::P * (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024) return 1;
+    return 0;
+}
+template <int LOGN, typename W>
+constexpr int ctmul_occ() {
+    constexpr int NL = ctmul_lds_slots<LOGN, W>();
+    return Geo<LOGN>::template occ_waves<W, NL * Geo<LOGN>::P * Geo<LOGN>::N>();
+}
+
+template <int LOGN, typename W, bool NEGA, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ctmul_occ<LOGN, W>()))
+k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *out, size_t batch,
+         NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    constexpr int NL = ctmul_lds_slots<LOGN, W>();
+    __shared__ W lds_all[G::P * G::LW + NL * G::P * G::N];
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t poly = (size_t)blockIdx.x * G::P + pl;
+    const bool valid = poly < batch;
+    if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped
+    W *lds = lds_all + pl * G::LW;
+    const uint64_t *xr = x + poly * 2 * G::N, *yr = y + poly * 2 * G::N;
+    uint64_t *orow = out + poly * 3 * G::N;
+    W creg[NL == 0 ? G::E : 1];
+    // slot s at global index gi (own positions only)
+    auto ld = [&](int s, uint32_t gi, int e) -> W {
+        if (NL == 3 || (NL == 1 && s == 2)) return lds_all[G::P * G::LW + ((NL == 3 ? s : 0) * G::P + pl) * G::N + gi];
+        if (s == 2) return creg[NL == 0 ? e : 0];
+        return valid ? (W)orow[(size_t)(s + 1) * G::N + gi] : W(0);
+    };
+    auto st = [&](int s, uint32_t gi, int e, W val) {
+        if (NL == 3 || (NL == 1 && s == 2)) lds_all[G::P * G::LW + ((NL == 3 ? s : 0) * G::P + pl) * G::N + gi] = val;
+        else if (s == 2) creg[NL == 0 ? e : 0] = val;
+        else if (valid) orow[(size_t)(s + 1) * G::N + gi] = (uint64_t)val;
+    };
+    constexpr int SA = 0, SB = 1, SC = 2;
+    W v[G::E];
+    // a fresh opaque copy of the lane index per phase: stops the compiler
+    // from keeping one phase's address arithmetic live across the next
+    // transform (scratch spills at N = 16384 otherwise)
+    auto lane = [&]() {
+        uint32_t t = tau;
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+
+    // 1. A = X0
+    uint32_t tp = lane();
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr, valid, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) st(SA, gidx<LOGN, G::NP - 1>(tp, e), e, fwd_to_canon<LAZY>(v[e], A));
+    if constexpr (G::NP > 1) __syncthreads();
+
+    // 2. Y0: B = Y0, c0 = inv(X0 Y0)
+    tp = lane();
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr, valid, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
+        const W y0 = v[e];
+        st(SB, gi, e, fwd_to_canon<LAZY>(y0, A));
+        v[e] = A.ar.mont(ld(SA, gi, e), y0);
+    }
+    __syncthreads();
+    tp = lane();
+    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow, valid, A, A.ninv_r, A.untwist_r);
+    __syncthreads();
+
+    // 3. X1: C = X1 Y0, B = X1
+    tp = lane();
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr + G::N, valid, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
+        const W x1 = v[e];
+        st(SC, gi, e, A.ar.mont(ld(SB, gi, e), x1));
+        st(SB, gi, e, fwd_to_canon<LAZY>(x1, A));
+    }
+    if constexpr (G::NP > 1) __syncthreads();
+
+    // 4. Y1: c1 = C + X0 Y1, C = X1 Y1
+    tp = lane();
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr + G::N, valid, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
+        const W y1 = v[e];
+        const W c1 = A.ar.red2q(ld(SC, gi, e) + A.ar.mont(ld(SA, gi, e), y1));
+        st(SC, gi, e, A.ar.mont(ld(SB, gi, e), y1));
+        v[e] = c1;
+    }
+    __syncthreads();  // every slot read of rows 1/2 precedes their final stores
+    tp = lane();
+    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow + G::N, valid, A, A.ninv_r, A.untwist_r);
+    __syncthreads();
+    tp = lane();
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) v[e] = ld(SC, gidx<LOGN, G::NP - 1>(tp, e), e);
+    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow + 2 * G::N, valid, A, A.ninv_r, A.untwist_r);
+}
+
+template <int LOGN, typename W, bool NEGA>
+static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *x, const uint64_t *y, uint64_t *out,
+                            size_t batch) {
+    using G = Geo<LOGN>;
+    const size_t blocks = (batch + G::P - 1) / G::P;
+    bool lazy = false;
+    if constexpr (sizeof(W) == 4) lazy = p.lazy;
+    if (lazy) {
+        if constexpr (sizeof(W) == 4)
+            hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
+                               batch, A);
+    } else
+        hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, false>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
+                           batch, A);
+    return hipGetLastError();
+}
+
+template <typename W, bool NEGA>
+static hipError_t ctmul_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_t *x, const uint64_t *y,
+                                 uint64_t *out, size_t batch) {
+    switch (p.logn) {
+#define FHE_CASE(L) \
+    case L: return ctmul_one<L, W, NEGA>(p, A, x, y, out, batch);
+        FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
+        FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
+#undef FHE_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_ct_mul(const Plan &p, const uint64_t *x, const uint64_t *y, uint64_t *out, size_t batch) {
+    if (batch == 0) return hipSuccess;
+    if (p.word == 32)
+        return p.nega ? ctmul_dispatch<uint32_t, true>(p, p.a32, x, y, out, batch)
+                      : ctmul_dispatch<uint32_t, false>(p, p.a32, x, y, out, batch);
+    return p.nega ? ctmul_dispatch<uint64_t, true>(p, p.a64, x, y, out, batch)
+                  : ctmul_dispatch<uint64_t, false>(p, p.a64, x, y, out, batch);
+}
+
+}  // namespace FHE_NS

@@ -444,10 +444,16 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
 // N^-1 * R; post = the matching negacyclic post-twist table.
 // Sub-transform use (ntt_big.hip): output i goes to dst[i << sh], global
 // index (i << sh) | off for the post-twist.
-template <int LOGN, bool NEGA, int PF = kPfSingle, typename W>
+// fin(gi, x): final map of canonical output x at global index gi (an
+// epilogue fused into the store, e.g. "+ c0" of a relinearisation).
+struct NoFin {
+    __device__ uint64_t operator()(uint32_t, uint64_t x) const { return x; }
+};
+template <int LOGN, bool NEGA, int PF = kPfSingle, typename W, typename F = NoFin>
 __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, uint64_t *__restrict__ dst,
                                                    bool valid, const NttArgs<W> &A, Tw<W> scale,
-                                                   const Tw<W> *__restrict__ post, uint32_t sh = 0, uint32_t off = 0) {
+                                                   const Tw<W> *__restrict__ post, uint32_t sh = 0, uint32_t off = 0,
+                                                   F &&fin = NoFin{}) {
     using G = Geo<LOGN>;
     constexpr int LAST = G::NP - 1;
     {
@@ -461,10 +467,11 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
         const uint32_t gi = (tau + cbrv(t, G::LOGE) * G::T) << sh;
         W x = v[t];
         if constexpr (NEGA) x = A.ar.shoup(x, post[gi | off]);
+        const uint64_t y = fin(gi, (uint64_t)A.ar.red1q(x));
         if constexpr (G::P == 1)
-            bstore(brsrc(dst), (tau << sh) * 8u, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u, (uint64_t)A.ar.red1q(x));
+            bstore(brsrc(dst), (tau << sh) * 8u, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u, y);
         else if (valid)
-            __builtin_nontemporal_store((uint64_t)A.ar.red1q(x), dst + gi);
+            __builtin_nontemporal_store(y, dst + gi);
     }
 }
 

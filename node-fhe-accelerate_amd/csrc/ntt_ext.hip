@@ -1,27 +1,45 @@
-// ntt_ext.hip -- TFHE external product (BootstrapEngine::external_product,
-// bootstrap_engine.cpp:431-518) for a batch of GLWE ciphertexts against one
-// GGSW key.
+// ntt_ext.hip -- decompose / NTT / key-MAC / inverse kernels: the TFHE
+// external product, BFV-style relinearisation and the blind-rotation CMux
+// step share one kernel body (k_dmac) and differ only in where the digit
+// polynomials come from and what the store epilogue adds.
 //
-// The reference computes, for each decomposition row r (mask polynomials
-// first, then the body; digit level inner, decompose_polynomial :152-185)
-// and each output component j:  res_j = mod_add(res_j,
-//   inv( fwd(decomp_r) (.) fwd(ggsw[r][j]) ))
-// i.e. (k+1)L + 2(k+1)^2 L transforms.  Because every intermediate is a
-// canonical residue and the inverse transform is linear over Z_q,
-//   sum_r inv(X_r) == inv(sum_r X_r)   (bit-exact),
-// so here: the GGSW is transformed once (fhe_ggsw_prepare, kept in NTT +
-// Montgomery form), every digit polynomial is decomposed on its HBM load,
-// transformed in registers/LDS, multiplied into (k+1) NTT-domain
-// accumulators held in VGPRs, and only (k+1) inverse transforms run at the
-// end -- (k+1)L + (k+1) transforms, one kernel, one HBM pass over the GLWE.
+// MODE 0  external product (BootstrapEngine::external_product,
+//         bootstrap_engine.cpp:431-518): for each decomposition row r (mask
+//         polynomials first, then the body; digit level inner, digits of
+//         decompose_polynomial :152-185) and each output component j:
+//           res_j = mod_add(res_j, inv( fwd(decomp_r) (.) fwd(ggsw[r][j]) )).
+// MODE 1  relinearisation (EncryptionEngine::relinearize, encryption.cpp:
+//         904-980): digit l of c2 is (c2 >> l*B) & (2^B - 1) (unsigned, LSB
+//         first); c0' = c0 + sum_l inv(fwd(d_l) (.) fwd(b_l)),
+//         c1' = c1 + sum_l inv(fwd(d_l) (.) fwd(a_l)), keys given as (a_l, b_l)
+//         pairs (KeySwitchKey, key_manager.h:85-95; key_manager.cpp:296-324).
+// MODE 2  one blind-rotation step (BootstrapEngine::blind_rotate :547-577 ->
+//         cmux :520-540 -> multiply_glwe_by_monomial :249-261 ->
+//         rotate_polynomial :122-145) for a batch of accumulators, each with
+//         its own LWE mask coefficient a_i:
+//           rot = (int32)((a_i * 2N + q/2) / q)   (u64 arithmetic)
+//           rot == 0 : acc unchanged (the reference `continue`s)
+//           else     : acc' = acc + ExtProd(X^rot * acc - acc, bsk[i])
+//         The rotation and the subtraction are folded into the digit load.
+// MODE 3  CMux with explicit inputs (cmux :520-540): out = ct0 +
+//         ExtProd(ct1 - ct0, ggsw).
+//
+// Every intermediate is a canonical residue and the inverse transform is
+// linear over Z_q, so  sum_r inv(X_r) == inv(sum_r X_r)  bit-exactly: keys are
+// transformed once (fhe_ggsw_prepare / fhe_relin_key_prepare: NTT x R,
+// Montgomery form), every digit polynomial is produced on its HBM load,
+// transformed in registers/LDS, multiplied into K1 NTT-domain accumulators,
+// and only K1 inverse transforms run at the end -- one kernel, one HBM pass
+// over the ciphertext.
 #include "fhe_internal.hpp"
+#include "lwe_ops.hpp"
 
 namespace FHE_NS {
 
-// Where the (k+1) NTT-domain accumulators live between rows: 1 = a second
-// LDS region, 2 = the ciphertext's own output rows in HBM (read-modify-write
-// of the thread's own positions; no synchronisation needed).  Holding them
-// in VGPRs spilled 300-800 B/lane.
+// Where the K1 NTT-domain accumulators live between rows: 1 = a second LDS
+// region, 2 = the ciphertext's own output rows in HBM (read-modify-write of
+// the thread's own positions; no synchronisation needed).  Holding them in
+// VGPRs spilled 300-800 B/lane.
 template <int LOGN, typename W, int K1>
 constexpr int ext_stash() {
     using G = Geo<LOGN>;
@@ -38,46 +56,77 @@ constexpr int ext_occ() {
     return Geo<LOGN>::template occ_waves<W, extra>();
 }
 
-template <int LOGN, typename W, bool NEGA, int K1, bool LAZY>
+struct DmArgs {
+    const uint64_t *src;    // MODE 0: glwe [batch][K1][N]; 1: ct [batch][3][N]; 2: acc [batch][K1][N]
+    const uint64_t *key;    // prepared key rows (NTT x R): 0/2: [K1*L][K1][N]; 1: [L][2][N] (a_l, b_l)
+    uint64_t *out;          // [batch][K1][N]
+    size_t batch;
+    int level, base_log;
+    const uint64_t *lwe_a;  // MODE 2: LWE masks [batch][lwe_dim]
+    uint64_t lwe_q;
+    uint32_t lwe_dim, step;
+    const uint64_t *src2;   // MODE 3: ct1 [batch][K1][N] (src = ct0)
+};
+
+template <int LOGN, typename W, bool NEGA, int K1, bool LAZY, int MODE>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ext_occ<LOGN, W, K1>()))
-k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, uint64_t *out,
-          size_t batch, int level, int base_log, NttArgs<W> A) {
+k_dmac(DmArgs D, NttArgs<W> A) {
     using G = Geo<LOGN>;
     constexpr int STASH = ext_stash<LOGN, W, K1>();
+    constexpr int NIN = MODE == 1 ? 3 : K1;  // source polynomials per ciphertext
     __shared__ W lds_all[G::P * G::LW + ext_extra_words<LOGN, W, K1>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
-    const bool valid = poly < batch;
+    const bool valid = poly < D.batch;
     if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped
     W *lds = lds_all + pl * G::LW;
-    uint64_t *orow = out + poly * K1 * G::N;
+    uint64_t *orow = D.out + poly * K1 * G::N;
+    const uint64_t *srow = D.src + (valid ? poly : 0) * NIN * G::N;
     // accumulator j of this ciphertext: LDS, or row j of the output
     auto acc = [&](int j) -> W * {
         if constexpr (STASH == 1) return lds_all + G::P * G::LW + (pl * K1 + j) * G::N;
         else return reinterpret_cast<W *>(orow + (size_t)j * G::N);
     };
 
-    const uint64_t base = 1ull << base_log, mask = base - 1, half = base / 2;
-    const uint64_t q = A.q64, lim = (uint64_t)A.ar.q2 * 2;
-    const int rows = K1 * level;
+    const int level = D.level;
+    const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    const uint64_t q = A.q64, mu = A.mu64, lim = (uint64_t)A.ar.q2 * 2;
+    bool skip = false;   // MODE 2, rot == 0: output = input accumulator
+    uint32_t rot = 0;
+    if constexpr (MODE == 2) {
+        const int32_t r = valid ? rot_amount(D.lwe_a[poly * D.lwe_dim + D.step], G::N, D.lwe_q) : 0;
+        skip = r == 0;
+        rot = rot_norm(r, G::N);
+        if (G::P == 1 && skip) {  // workgroup-uniform: copy and leave
+            for (uint32_t i = threadIdx.x; i < (uint32_t)(K1 * G::N); i += G::THREADS) orow[i] = srow[i];
+            return;
+        }
+    }
+    const int rows = MODE == 1 ? level : K1 * level;
     for (int r = 0; r < rows; ++r) {
         // opaque per-row copy of the lane index: keeps the (loop-invariant)
         // address arithmetic inside the loop instead of 100+ hoisted VGPRs
         uint32_t tr = tau;
         asm volatile("" : "+v"(tr));
-        const int i = r / level, l = r % level;
-        const uint32_t shift = uint32_t(level - 1 - l) * uint32_t(base_log);
-        const uint64_t *src = glwe + (poly * K1 + i) * G::N;
+        const int i = MODE == 1 ? 2 : r / level, l = MODE == 1 ? r : r % level;
+        const uint32_t shift = MODE == 1 ? uint32_t(l) * uint32_t(D.base_log)
+                                         : uint32_t(level - 1 - l) * uint32_t(D.base_log);
+        const uint64_t *src = srow + (size_t)i * G::N;
+        const uint64_t *src2 = MODE == 3 ? D.src2 + ((valid ? poly : 0) * K1 + i) * G::N : nullptr;
         if (r > 0 && G::NP > 1) __syncthreads();
         W v[G::E];
         Tw<W> t0[PassTw<LOGN, 0>::COUNT];
         load_tw<LOGN, 0>(tr, A.twf, t0);
-        load_coeffs<G::E>(v, lim, q, A.mu64, [&](int t) -> uint64_t {
-            const uint64_t c = valid ? src[tr + cbrv(t, G::LOGE) * G::T] : 0;
+        load_coeffs<G::E>(v, lim, q, mu, [&](int t) -> uint64_t {
+            const uint32_t p = tr + cbrv(t, G::LOGE) * G::T;
+            if (!valid || skip) return 0;
+            uint64_t c;
+            if constexpr (MODE == 2) c = subq(red_q(rotated_at(src, p, rot, G::N, q, mu), q, mu), red_q(src[p], q, mu), q);
+            else if constexpr (MODE == 3) c = subq(red_q(src2[p], q, mu), red_q(src[p], q, mu), q);
+            else c = src[p];
             uint64_t d = (c >> shift) & mask;
-            if (d > half) {
-                d = q - (base - d);
-                if (d >= q) d = mod64_slow(d, q, A.mu64);
+            if constexpr (MODE != 1) {
+                if (d > half) d = red_q(q - (base - d), q, mu);
             }
             return d;
         });
@@ -88,7 +137,7 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
         fwd_pass<LOGN, 0, LAZY>(v, t0, A.ar);
         fwd_rest<LOGN, 1, LAZY, kPfSingle>(lds, v, tr, A.twf, A.ar);
         if (!valid) continue;
-        const uint64_t *g = ggsw + (size_t)r * K1 * G::N;
+        const uint64_t *g = D.key + (size_t)r * K1 * G::N;
         // chunks of 2 coefficients: all key + accumulator loads of the row in
         // flight at once would not fit the register budget
 #pragma unroll
@@ -100,7 +149,8 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
 #pragma unroll
                 for (int j = 0; j < K1; ++j) {
                     const uint32_t gi = gidx<LOGN, G::NP - 1>(tr, c0 + e);
-                    kv[e][j] = g[(size_t)j * G::N + gi];
+                    const int kj = MODE == 1 ? 1 - j : j;  // relin: c0' uses b_l, c1' uses a_l
+                    kv[e][j] = g[(size_t)kj * G::N + gi];
                     pv[e][j] = r == 0 ? W(0) : acc(j)[gi];
                 }
 #pragma unroll
@@ -124,27 +174,36 @@ k_extprod(const uint64_t *__restrict__ glwe, const uint64_t *__restrict__ ggsw, 
         if constexpr (STASH == 2) {
             if (G::NP > 1) __syncthreads();  // every stash read of row j precedes its final stores
         }
-        inv_poly_from_regs<LOGN, NEGA>(lds, v, tr, orow + (size_t)j * G::N, valid, A, A.ninv, A.untwist);
+        // MODE 1: + c_j (mod_add of encryption.cpp:953/958); MODE 2: + acc_j
+        // (cmux's add_glwe_inplace, :537), or acc_j itself when skipped.
+        const uint64_t *addend = srow + (size_t)j * G::N;
+        auto fin = [&](uint32_t gi, uint64_t x) -> uint64_t {
+            if constexpr (MODE == 0) return x;
+            else {
+                if (!valid) return 0;
+                const uint64_t a = addend[gi];
+                if (MODE == 2 && skip) return a;
+                return addq(x, red_q(a, q, mu), q);
+            }
+        };
+        inv_poly_from_regs<LOGN, NEGA>(lds, v, tr, orow + (size_t)j * G::N, valid, A, A.ninv, A.untwist, 0, 0, fin);
     }
 }
 
-template <int LOGN, typename W, bool NEGA>
-static hipError_t ext_one(const NttArgs<W> &A, hipStream_t s, int k1, int level, int base_log, const uint64_t *glwe,
-                          const uint64_t *ggsw, uint64_t *out, size_t batch) {
+template <int LOGN, typename W, bool NEGA, int MODE>
+static hipError_t dmac_one(const NttArgs<W> &A, hipStream_t s, int k1, const DmArgs &D) {
     using G = Geo<LOGN>;
-    const size_t blocks = (batch + G::P - 1) / G::P;
+    const size_t blocks = (D.batch + G::P - 1) / G::P;
     if (k1 != 2) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_extprod<LOGN, W, NEGA, 2, false>), dim3(blocks), dim3(G::THREADS), 0, s, glwe, ggsw, out,
-                       batch, level, base_log, A);
+    hipLaunchKernelGGL((k_dmac<LOGN, W, NEGA, 2, false, MODE>), dim3(blocks), dim3(G::THREADS), 0, s, D, A);
     return hipGetLastError();
 }
 
-template <typename W, bool NEGA>
-static hipError_t ext_dispatch(const Plan &p, const NttArgs<W> &A, int k1, int level, int base_log,
-                               const uint64_t *glwe, const uint64_t *ggsw, uint64_t *out, size_t batch) {
+template <typename W, bool NEGA, int MODE>
+static hipError_t dmac_dispatch(const Plan &p, const NttArgs<W> &A, int k1, const DmArgs &D) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return ext_one<L, W, NEGA>(A, p.stream, k1, level, base_log, glwe, ggsw, out, batch);
+    case L: return dmac_one<L, W, NEGA, MODE>(A, p.stream, k1, D);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -152,14 +211,39 @@ static hipError_t ext_dispatch(const Plan &p, const NttArgs<W> &A, int k1, int l
     }
 }
 
+template <int MODE>
+static hipError_t dmac(const Plan &p, int k1, const DmArgs &D) {
+    if (D.batch == 0) return hipSuccess;
+    if (p.word == 32)
+        return p.nega ? dmac_dispatch<uint32_t, true, MODE>(p, p.a32, k1, D)
+                      : dmac_dispatch<uint32_t, false, MODE>(p, p.a32, k1, D);
+    return p.nega ? dmac_dispatch<uint64_t, true, MODE>(p, p.a64, k1, D)
+                  : dmac_dispatch<uint64_t, false, MODE>(p, p.a64, k1, D);
+}
+
 hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const uint64_t *glwe,
                           const uint64_t *ggsw, uint64_t *out, size_t batch) {
-    if (batch == 0) return hipSuccess;
-    if (p.word == 32)
-        return p.nega ? ext_dispatch<uint32_t, true>(p, p.a32, k1, level, base_log, glwe, ggsw, out, batch)
-                      : ext_dispatch<uint32_t, false>(p, p.a32, k1, level, base_log, glwe, ggsw, out, batch);
-    return p.nega ? ext_dispatch<uint64_t, true>(p, p.a64, k1, level, base_log, glwe, ggsw, out, batch)
-                  : ext_dispatch<uint64_t, false>(p, p.a64, k1, level, base_log, glwe, ggsw, out, batch);
+    DmArgs D{glwe, ggsw, out, batch, level, base_log, nullptr, 0, 0, 0, nullptr};
+    return dmac<0>(p, k1, D);
+}
+
+hipError_t launch_relin(const Plan &p, int level, int base_log, const uint64_t *ct3, const uint64_t *rlk,
+                        uint64_t *out, size_t batch) {
+    DmArgs D{ct3, rlk, out, batch, level, base_log, nullptr, 0, 0, 0, nullptr};
+    return dmac<1>(p, 2, D);
+}
+
+hipError_t launch_cmux_rotate(const Plan &p, int k1, int level, int base_log, const uint64_t *acc_in,
+                              const uint64_t *ggsw, uint64_t *acc_out, size_t batch, const uint64_t *lwe_a,
+                              uint32_t lwe_dim, uint32_t step, uint64_t lwe_q) {
+    DmArgs D{acc_in, ggsw, acc_out, batch, level, base_log, lwe_a, lwe_q, lwe_dim, step, nullptr};
+    return dmac<2>(p, k1, D);
+}
+
+hipError_t launch_cmux(const Plan &p, int k1, int level, int base_log, const uint64_t *ggsw, const uint64_t *ct0,
+                       const uint64_t *ct1, uint64_t *out, size_t batch) {
+    DmArgs D{ct0, ggsw, out, batch, level, base_log, nullptr, 0, 0, 0, ct1};
+    return dmac<3>(p, k1, D);
 }
 
 }  // namespace FHE_NS

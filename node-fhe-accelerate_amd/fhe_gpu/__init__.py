@@ -14,6 +14,10 @@ ModularArithmetic              :class:`ModularArithmetic` (modular_arithmetic.h:
 BarrettReducer                 :class:`BarrettReducer` (modular_arithmetic.h:82-)
 MultiLimbModularArithmetic     :class:`MultiLimbModularArithmetic`
 BootstrapEngine::external_product  :class:`ExternalProduct`
+BootstrapEngine (cmux, blind_rotate, :class:`BootstrapEngine`
+  sample_extract, key_switch, ...)
+EncryptionEngine::multiply /   :class:`EncryptionEngine`, :class:`EvaluationKey`
+  relinearize / multiply_relin
 HardwareDetector::detect       :func:`detect_hardware`
 =============================  ==============================================
 
@@ -107,6 +111,19 @@ SIGNATURES = [
     ("fhe_external_product_batch", C.c_int,
      [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
     ("fhe_decompose_batch", C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_ct_multiply_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int, C.c_int]),
+    ("fhe_relin_key_prepare", C.c_int, [vp, C.c_uint32, vp, vp, C.c_int]),
+    ("fhe_relinearize_batch", C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_ct_multiply_relin_batch", C.c_int,
+     [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_glwe_rotate_batch", C.c_int, [vp, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_cmux_batch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_blind_rotate_batch", C.c_int,
+     [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint64, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_sample_extract_batch", C.c_int, [vp, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_key_switch_batch", C.c_int,
+     [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp, C.c_size_t, C.c_int,
+      C.c_int, vp]),
     ("fhe_modmul_batch", C.c_int, [C.c_uint64, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
     ("fhe_ml_constants", C.c_int, [u64p, u64p]),
     ("fhe_ml_montmul_batch", C.c_int, [u64p, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
@@ -437,6 +454,212 @@ class ExternalProduct:
         _check(lib().fhe_external_product_batch(self.ring._h, self.k, self.base_log, self.level, bi.ptr, bk.ptr,
                                                 bo.ptr, nb, w))
         return out
+
+
+def _empty(like, shape):
+    if _is_tensor(like):
+        return torch.empty(shape, dtype=like.dtype, device=like.device)
+    return np.empty(shape, dtype=np.uint64)
+
+
+def _lead(x, tail) -> int:
+    """Batch size of x with trailing shape `tail`."""
+    shape = tuple(x.shape)
+    if len(shape) < len(tail) or shape[len(shape) - len(tail):] != tuple(tail):
+        raise FHEError(-9, f"expected shape [..., {', '.join(map(str, tail))}], got {list(shape)}")
+    return int(np.prod(shape[: len(shape) - len(tail)])) if len(shape) > len(tail) else 1
+
+
+class EvaluationKey:
+    """Relinearisation key (KeySwitchKey of key_manager.h:85-111): the
+    (a_l, b_l) pairs ``rlk`` [level, 2, n] in coefficient form, prepared once
+    into the NTT domain on the GPU."""
+
+    def __init__(self, ring: "PolynomialRing", rlk, decomp_base_log: int = 0):
+        rlk = _as_u64(rlk)
+        self.level = int(rlk.shape[0]) if rlk.ndim == 3 else 0
+        if self.level and tuple(rlk.shape[1:]) != (2, ring.degree):
+            raise FHEError(-9, "rlk must have shape [level, 2, n]")
+        # encryption.cpp:935: base_log 0 -> 4
+        self.decomp_base_log = decomp_base_log if decomp_base_log > 0 else 4
+        self.ring = ring
+        self.rlk_ntt = _like(rlk)
+        if self.level:
+            bi, bo = _Buf(rlk), _Buf(self.rlk_ntt, True)
+            w = _where(bi, bo)
+            ring._bind_stream(w)
+            _check(lib().fhe_relin_key_prepare(ring._h, self.level, bi.ptr, bo.ptr, w))
+
+
+class EncryptionEngine:
+    """Ciphertext arithmetic of EncryptionEngine (encryption.cpp:594-980) over
+    batches of ciphertexts [..., 2, n] (c0, c1) / [..., 3, n] (degree 2)."""
+
+    def __init__(self, ring: "PolynomialRing"):
+        self.ring = ring
+
+    def multiply(self, ct1, ct2, is_ntt: bool = False, out=None):
+        """multiply (:737-798): tensor product -> [..., 3, n]."""
+        r = self.ring
+        ct1, ct2 = _as_u64(ct1), _as_u64(ct2)
+        nb = _lead(ct1, (2, r.degree))
+        if tuple(ct2.shape) != tuple(ct1.shape):
+            raise FHEError(-9, "ciphertext shapes differ")
+        if out is None:
+            out = _empty(ct1, tuple(ct1.shape[:-2]) + (3, r.degree))
+        b1, b2, bo = _Buf(ct1), _Buf(ct2), _Buf(out, True)
+        w = _where(b1, b2, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_ct_multiply_batch(r._h, b1.ptr, b2.ptr, bo.ptr, nb, int(bool(is_ntt)), w))
+        return out
+
+    def relinearize(self, ct3, ek: EvaluationKey, out=None):
+        """relinearize (:904-980): [..., 3, n] -> [..., 2, n]."""
+        r = self.ring
+        ct3 = _as_u64(ct3)
+        nb = _lead(ct3, (3, r.degree))
+        if out is None:
+            out = _empty(ct3, tuple(ct3.shape[:-2]) + (2, r.degree))
+        bi, bk, bo = _Buf(ct3), _Buf(ek.rlk_ntt), _Buf(out, True)
+        w = _where(bi, bo) if not ek.level else _where(bi, bk, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_relinearize_batch(r._h, ek.decomp_base_log, ek.level, bi.ptr, bk.ptr if ek.level else None,
+                                           bo.ptr, nb, w))
+        return out
+
+    def multiply_relin(self, ct1, ct2, ek: EvaluationKey, out=None):
+        """multiply_relin (:800-807)."""
+        r = self.ring
+        ct1, ct2 = _as_u64(ct1), _as_u64(ct2)
+        nb = _lead(ct1, (2, r.degree))
+        if tuple(ct2.shape) != tuple(ct1.shape):
+            raise FHEError(-9, "ciphertext shapes differ")
+        out = _like(ct1) if out is None else out
+        b1, b2, bk, bo = _Buf(ct1), _Buf(ct2), _Buf(ek.rlk_ntt), _Buf(out, True)
+        w = _where(b1, b2, bo) if not ek.level else _where(b1, b2, bk, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_ct_multiply_relin_batch(r._h, ek.decomp_base_log, ek.level, b1.ptr, b2.ptr,
+                                                 bk.ptr if ek.level else None, bo.ptr, nb, w))
+        return out
+
+
+class BootstrapEngine:
+    """The TFHE pieces of BootstrapEngine (bootstrap_engine.cpp) batched over
+    ciphertexts: GLWE [..., k+1, n], GGSW [(k+1)*level, k+1, n], LWE masks
+    [..., dim] with bodies [...]."""
+
+    def __init__(self, ring: NTTProcessor, base_log: int, level: int, k: int = 1):
+        self.ring, self.base_log, self.level, self.k = ring, base_log, level, k
+
+    def prepare_ggsw(self, ggsw):
+        """GGSW(s) [..., (k+1)*level, k+1, n] -> NTT-domain form (same shape)."""
+        r, k, L = self.ring, self.k, self.level
+        g = _as_u64(ggsw)
+        nb = _lead(g, ((k + 1) * L, k + 1, r.degree))
+        out = _like(g)
+        bi, bo = _Buf(g), _Buf(out, True)
+        w = _where(bi, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_ggsw_prepare(r._h, k, L * nb, bi.ptr, bo.ptr, w))
+        return out
+
+    def external_product(self, glwe, ggsw_ntt, out=None):
+        r = self.ring
+        glwe = _as_u64(glwe)
+        nb = _lead(glwe, (self.k + 1, r.degree))
+        out = _like(glwe) if out is None else out
+        bi, bk, bo = _Buf(glwe), _Buf(ggsw_ntt), _Buf(out, True)
+        w = _where(bi, bk, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_external_product_batch(r._h, self.k, self.base_log, self.level, bi.ptr, bk.ptr, bo.ptr,
+                                                nb, w))
+        return out
+
+    def cmux(self, ggsw_ntt, ct0, ct1, out=None):
+        """cmux (:520-540): ct0 + ggsw (x) (ct1 - ct0)."""
+        r = self.ring
+        ct0, ct1 = _as_u64(ct0), _as_u64(ct1)
+        nb = _lead(ct0, (self.k + 1, r.degree))
+        if tuple(ct1.shape) != tuple(ct0.shape):
+            raise FHEError(-9, "ciphertext shapes differ")
+        out = _like(ct0) if out is None else out
+        bg, b0, b1, bo = _Buf(ggsw_ntt), _Buf(ct0), _Buf(ct1), _Buf(out, True)
+        w = _where(bg, b0, b1, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_cmux_batch(r._h, self.k, self.base_log, self.level, bg.ptr, b0.ptr, b1.ptr, bo.ptr, nb, w))
+        return out
+
+    def multiply_glwe_by_monomial(self, glwe, rotation, out=None):
+        """multiply_glwe_by_monomial (:249-261); rotation: one int per ciphertext."""
+        r = self.ring
+        glwe = _as_u64(glwe)
+        nb = _lead(glwe, (self.k + 1, r.degree))
+        if _is_tensor(glwe):
+            rot = torch.as_tensor(rotation, dtype=torch.int32, device=glwe.device).reshape(-1).contiguous()
+            rp = rot.data_ptr()
+        else:
+            rot = np.ascontiguousarray(np.asarray(rotation, dtype=np.int32).reshape(-1))
+            rp = rot.ctypes.data
+        cnt = rot.numel() if _is_tensor(rot) else rot.size
+        if cnt != nb:
+            raise FHEError(-9, "one rotation per ciphertext")
+        out = _like(glwe) if out is None else out
+        bi, bo = _Buf(glwe), _Buf(out, True)
+        w = _where(bi, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_glwe_rotate_batch(r._h, self.k, rp, bi.ptr, bo.ptr, nb, w))
+        return out
+
+    def blind_rotate(self, acc, lwe_a, lwe_b, bsk_ntt, lwe_q: Optional[int] = None):
+        """blind_rotate (:547-577), in place on acc [..., k+1, n]; lwe_a
+        [..., dim], lwe_b [...]; bsk_ntt [dim, (k+1)*level, k+1, n] from
+        prepare_ggsw.  lwe_q defaults to the ring modulus (:39-40)."""
+        r = self.ring
+        acc, lwe_a, lwe_b = _as_u64(acc), _as_u64(lwe_a), _as_u64(lwe_b)
+        nb = _lead(acc, (self.k + 1, r.degree))
+        dim = int(lwe_a.shape[-1])
+        ba, bla, blb, bk = _Buf(acc, True), _Buf(lwe_a), _Buf(lwe_b), _Buf(bsk_ntt)
+        if bla.count != nb * dim or blb.count != nb:
+            raise FHEError(-9, "LWE masks must be [batch, dim] and bodies [batch]")
+        w = _where(ba, bla, blb, bk)
+        r._bind_stream(w)
+        _check(lib().fhe_blind_rotate_batch(r._h, self.k, self.base_log, self.level, dim, bla.ptr, blb.ptr,
+                                            lwe_q if lwe_q is not None else r.modulus, bk.ptr, ba.ptr, nb, w))
+        return acc
+
+    def sample_extract(self, glwe):
+        """sample_extract (:594-624) -> (a [..., k*n], b [...])."""
+        r = self.ring
+        glwe = _as_u64(glwe)
+        nb = _lead(glwe, (self.k + 1, r.degree))
+        lead = tuple(glwe.shape[:-2])
+        a = _empty(glwe, lead + (self.k * r.degree,))
+        b = _empty(glwe, lead if lead else (1,))
+        bi, ba, bb = _Buf(glwe), _Buf(a, True), _Buf(b, True)
+        w = _where(bi, ba, bb)
+        r._bind_stream(w)
+        _check(lib().fhe_sample_extract_batch(r._h, self.k, bi.ptr, ba.ptr, bb.ptr, nb, w))
+        return a, b
+
+    @staticmethod
+    def key_switch(q: int, base_log: int, level: int, ksk_a, ksk_b, lwe_a, lwe_b, device: int = 0):
+        """key_switch (:630-677): ksk_a [in_dim*level, out_dim], ksk_b
+        [in_dim*level]; lwe_a [..., in_dim], lwe_b [...] -> (a, b)."""
+        ksk_a, ksk_b, lwe_a, lwe_b = (_as_u64(x) for x in (ksk_a, ksk_b, lwe_a, lwe_b))
+        in_dim = int(lwe_a.shape[-1])
+        out_dim = int(ksk_a.shape[-1])
+        nb = _lead(lwe_a, (in_dim,))
+        out_a = _empty(lwe_a, tuple(lwe_a.shape[:-1]) + (out_dim,))
+        out_b = _like(lwe_b)
+        bka, bkb, bla, blb, boa, bob = (_Buf(ksk_a), _Buf(ksk_b), _Buf(lwe_a), _Buf(lwe_b), _Buf(out_a, True),
+                                        _Buf(out_b, True))
+        if bka.count != in_dim * level * out_dim or bkb.count != in_dim * level or blb.count != nb:
+            raise FHEError(-9, "key switching key / LWE shapes disagree")
+        w = _where(bka, bkb, bla, blb, boa, bob)
+        s = _stream_ptr() if w == FHE_DEVICE else None
+        _check(lib().fhe_key_switch_batch(q, base_log, level, in_dim, out_dim, bka.ptr, bkb.ptr, bla.ptr, blb.ptr,
+                                          boa.ptr, bob.ptr, nb, w, device, s))
+        return out_a, out_b
 
 
 def decompose_polynomial(ring: NTTProcessor, poly, base_log: int, level: int, out=None):

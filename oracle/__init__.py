@@ -80,6 +80,13 @@ def lib():
         L.oracle_external_product.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p, u64p]
         L.oracle_rotate.argtypes = [C.c_uint64, u64p, C.c_uint32, C.c_int32, u64p]
         L.oracle_sample_extract.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, u64p, u64p, u64p]
+        L.oracle_cmux.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p, u64p, u64p]
+        L.oracle_blind_rotate.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u64p,
+                                          C.c_uint64, C.c_uint64, u64p, u64p]
+        L.oracle_key_switch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p,
+                                        u64p, C.c_uint64, u64p, u64p]
+        L.oracle_ct_multiply.argtypes = [C.c_void_p, u64p, u64p, C.c_int, u64p]
+        L.oracle_relinearize.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, u64p, u64p, u64p]
         L.oracle_testrandom_coeffs.argtypes = [C.c_uint64, C.c_uint64, u64p, C.c_size_t]
         L.oracle_mt19937_64_raw.argtypes = [C.c_uint64, u64p, C.c_size_t]
         L.oracle_splitmix_fill.argtypes = [C.c_uint64, C.c_uint64, u64p, C.c_size_t, C.c_size_t]
@@ -244,6 +251,19 @@ def sample_extract(q, glwe):
     return a, b.value
 
 
+def key_switch(q, base_log, level, ksk_a, ksk_b, lwe_a, lwe_b):
+    """BootstrapEngine::key_switch for one LWE ciphertext -> (out_a, out_b)."""
+    ksk_a = np.ascontiguousarray(ksk_a, dtype=np.uint64)
+    ksk_b = np.ascontiguousarray(ksk_b, dtype=np.uint64)
+    lwe_a = np.ascontiguousarray(lwe_a, dtype=np.uint64)
+    out_dim = ksk_a.shape[1]
+    out_a = np.empty(out_dim, dtype=np.uint64)
+    b = C.c_uint64()
+    lib().oracle_key_switch(q, base_log, level, lwe_a.size, out_dim, _p(ksk_a), _p(ksk_b), _p(lwe_a), lwe_b,
+                            _p(out_a), C.byref(b))
+    return out_a, b.value
+
+
 def testrandom_coeffs(seed, q, count):
     out = np.empty(count, dtype=np.uint64)
     lib().oracle_testrandom_coeffs(seed, q, _p(out), count)
@@ -326,6 +346,31 @@ class NTT:
         ggsw = np.ascontiguousarray(ggsw, dtype=np.uint64)
         out = np.empty(((k + 1), self.n), dtype=np.uint64)
         lib().oracle_external_product(self._h, k, base_log, level, _p(glwe), _p(ggsw), _p(out))
+        return out
+
+    def cmux(self, k, base_log, level, ggsw, ct0, ct1):
+        ggsw, ct0, ct1 = (np.ascontiguousarray(x, dtype=np.uint64) for x in (ggsw, ct0, ct1))
+        out = np.empty(((k + 1), self.n), dtype=np.uint64)
+        lib().oracle_cmux(self._h, k, base_log, level, _p(ggsw), _p(ct0), _p(ct1), _p(out))
+        return out
+
+    def blind_rotate(self, k, base_log, level, lwe_a, lwe_b, lwe_q, bsk, acc):
+        lwe_a, bsk = (np.ascontiguousarray(x, dtype=np.uint64) for x in (lwe_a, bsk))
+        acc = np.array(acc, dtype=np.uint64, copy=True, order="C")
+        lib().oracle_blind_rotate(self._h, k, base_log, level, lwe_a.size, _p(lwe_a), lwe_b, lwe_q, _p(bsk), _p(acc))
+        return acc
+
+    def ct_multiply(self, ct1, ct2, is_ntt=False):
+        ct1, ct2 = (np.ascontiguousarray(x, dtype=np.uint64) for x in (ct1, ct2))
+        out = np.empty((3, self.n), dtype=np.uint64)
+        lib().oracle_ct_multiply(self._h, _p(ct1), _p(ct2), int(is_ntt), _p(out))
+        return out
+
+    def relinearize(self, base_log, level, ct3, rlk):
+        ct3 = np.ascontiguousarray(ct3, dtype=np.uint64)
+        rlk = np.ascontiguousarray(rlk, dtype=np.uint64) if level else np.zeros(1, dtype=np.uint64)
+        out = np.empty((2, self.n), dtype=np.uint64)
+        lib().oracle_relinearize(self._h, base_log, level, _p(ct3), _p(rlk), _p(out))
         return out
 
     def batch_threaded(self, op, a, b=None, c=None, threads=1):

@@ -554,6 +554,113 @@ void oracle_sample_extract(u64 q, u32 k, u32 n, const u64 *glwe, u64 *a, u64 *b)
     *b = glwe[(size_t)k * n];
 }
 
+/* cmux (:520-540): diff = ct1 - ct0 (subtract_glwe_inplace -> mod_sub),
+ * product = external_product(diff, ggsw), product += ct0 (mod_add). */
+void oracle_cmux(const oracle_ntt *t, u32 k, u32 base_log, u32 level, const u64 *ggsw,
+                 const u64 *ct0, const u64 *ct1, u64 *out) {
+    const size_t m = (size_t)(k + 1) * t->n;
+    u64 *diff = (u64 *)calloc(m, sizeof(u64));
+    for (size_t x = 0; x < m; ++x) diff[x] = oracle_mod_sub(t->q, ct1[x], ct0[x]);
+    oracle_external_product(t, k, base_log, level, diff, ggsw, out);
+    for (size_t x = 0; x < m; ++x) out[x] = oracle_mod_add(t->q, out[x], ct0[x]);
+    free(diff);
+}
+
+/* multiply_glwe_by_monomial (:249-261): every polynomial rotated */
+static void glwe_rotate(u64 q, u32 k, u32 n, const u64 *in, int32_t r, u64 *out) {
+    for (u32 i = 0; i <= k; ++i) oracle_rotate(q, in + (size_t)i * n, n, r, out + (size_t)i * n);
+}
+
+/* blind_rotate (:547-577) of acc [(k+1)][n] in place; lwe_q = lwe_modulus_
+ * (= glwe modulus, :39-40); bsk: lwe_dim GGSWs [(k+1)*level][(k+1)][n]. */
+void oracle_blind_rotate(const oracle_ntt *t, u32 k, u32 base_log, u32 level, u32 lwe_dim,
+                         const u64 *lwe_a, u64 lwe_b, u64 lwe_q, const u64 *bsk, u64 *acc) {
+    const u32 n = t->n;
+    const size_t m = (size_t)(k + 1) * n, gw = (size_t)(k + 1) * level * (k + 1) * n;
+    u64 *rot = (u64 *)malloc(sizeof(u64) * m), *res = (u64 *)malloc(sizeof(u64) * m);
+    int32_t b_rotation = -(int32_t)((lwe_b * 2 * n + lwe_q / 2) / lwe_q);
+    glwe_rotate(t->q, k, n, acc, b_rotation, rot);
+    memcpy(acc, rot, sizeof(u64) * m);
+    for (u32 i = 0; i < lwe_dim; ++i) {
+        int32_t a_rotation = (int32_t)((lwe_a[i] * 2 * n + lwe_q / 2) / lwe_q);
+        if (a_rotation == 0) continue;
+        glwe_rotate(t->q, k, n, acc, a_rotation, rot);
+        oracle_cmux(t, k, base_log, level, bsk + gw * i, acc, rot, res);
+        memcpy(acc, res, sizeof(u64) * m);
+    }
+    free(rot); free(res);
+}
+
+/* key_switch (:630-677): ksk_a [in_dim*level][out_dim] (keys[idx].first),
+ * ksk_b [in_dim*level] (keys[idx].second[0]). */
+void oracle_key_switch(u64 q, u32 base_log, u32 level, u32 in_dim, u32 out_dim, const u64 *ksk_a,
+                       const u64 *ksk_b, const u64 *lwe_a, u64 lwe_b, u64 *out_a, u64 *out_b) {
+    u64 base = 1ULL << base_log, mask = base - 1;
+    memset(out_a, 0, sizeof(u64) * out_dim);
+    u64 rb = lwe_b;
+    size_t idx = 0;
+    for (u32 i = 0; i < in_dim; ++i) {
+        u64 coeff = lwe_a[i];
+        for (u32 l = 0; l < level; ++l) {
+            u32 shift = (level - 1 - l) * base_log;
+            u64 digit = (coeff >> shift) & mask;
+            if (digit == 0) { idx++; continue; }
+            const u64 *ka = ksk_a + idx * out_dim;
+            for (u32 j = 0; j < out_dim; ++j) out_a[j] = (out_a[j] + q - (digit * ka[j]) % q) % q;
+            rb = (rb + q - (digit * ksk_b[idx]) % q) % q;
+            idx++;
+        }
+    }
+    *out_b = rb;
+}
+
+/* EncryptionEngine::multiply (encryption.cpp:737-798): ct [2][n] each;
+ * out [3][n].  is_ntt: inputs already in the NTT domain (no transforms). */
+void oracle_ct_multiply(const oracle_ntt *t, const u64 *ct1, const u64 *ct2, int is_ntt, u64 *out) {
+    const u32 n = t->n; const u64 q = t->q;
+    u64 *w = (u64 *)malloc(sizeof(u64) * n * 6);
+    u64 *x0 = w, *x1 = w + n, *y0 = w + 2 * n, *y1 = w + 3 * n, *p = w + 4 * n, *r = w + 5 * n;
+    memcpy(x0, ct1, 8 * n); memcpy(x1, ct1 + n, 8 * n);
+    memcpy(y0, ct2, 8 * n); memcpy(y1, ct2 + n, 8 * n);
+    if (!is_ntt) {
+        oracle_ntt_forward(t, x0); oracle_ntt_forward(t, x1);
+        oracle_ntt_forward(t, y0); oracle_ntt_forward(t, y1);
+    }
+    oracle_pointwise(q, x0, y0, out, n);                /* c0 */
+    oracle_pointwise(q, x0, y1, p, n);                  /* c1 */
+    oracle_pointwise(q, x1, y0, r, n);
+    oracle_poly_add(q, p, r, out + n, n);
+    oracle_pointwise(q, x1, y1, out + 2 * n, n);        /* c2 */
+    if (!is_ntt) {
+        oracle_ntt_inverse(t, out); oracle_ntt_inverse(t, out + n); oracle_ntt_inverse(t, out + 2 * n);
+    }
+    free(w);
+}
+
+/* EncryptionEngine::relinearize (:904-980) with num_levels key pairs:
+ * ct3 [3][n]; rlk [level][2][n] as (a_l, b_l); out [2][n]. */
+void oracle_relinearize(const oracle_ntt *t, u32 base_log, u32 level, const u64 *ct3, const u64 *rlk, u64 *out) {
+    const u32 n = t->n; const u64 q = t->q;
+    u64 base = 1ULL << base_log, mask = base - 1;
+    u64 *d = (u64 *)malloc(sizeof(u64) * n * 4);
+    u64 *ka = d + n, *kb = d + 2 * n, *pr = d + 3 * n;
+    memcpy(out, ct3, 8 * (size_t)n * 2);
+    for (u32 l = 0; l < level; ++l) {
+        u64 shift = (u64)l * base_log;
+        for (u32 i = 0; i < n; ++i) d[i] = (ct3[2 * (size_t)n + i] >> shift) & mask;
+        memcpy(ka, rlk + (2 * (size_t)l) * n, 8 * n);
+        memcpy(kb, rlk + (2 * (size_t)l + 1) * n, 8 * n);
+        oracle_ntt_forward(t, d); oracle_ntt_forward(t, ka); oracle_ntt_forward(t, kb);
+        oracle_pointwise(q, d, kb, pr, n);
+        oracle_ntt_inverse(t, pr);
+        oracle_poly_add(q, out, pr, out, n);
+        oracle_pointwise(q, d, ka, pr, n);
+        oracle_ntt_inverse(t, pr);
+        oracle_poly_add(q, out + n, pr, out + n, n);
+    }
+    free(d);
+}
+
 /* ------------------------------------------------------------------------
  * Test-input generators
  * ------------------------------------------------------------------------ */

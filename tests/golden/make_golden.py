@@ -173,11 +173,48 @@ def negacyclic():
     return out
 
 
+def cipher():
+    """Ciphertext-level vectors (EncryptionEngine::multiply / relinearize,
+    BootstrapEngine::blind_rotate) from the C restatement; the multiply
+    vectors are cross-checked against pyref's independent transform."""
+    out = []
+    for n, q in [(16, 97), (256, 7681), (1024, P27), (1024, P62)]:
+        t = oracle.NTT(n, q)
+        x = oracle.testrandom_coeffs(21, q, 2 * n).reshape(2, n)
+        y = oracle.testrandom_coeffs(22, q, 2 * n).reshape(2, n)
+        res = t.ct_multiply(x, y)
+        if n <= 256:
+            xs, ys = [L(v) for v in x], [L(v) for v in y]
+            c1 = [(a + b) % q for a, b in zip(pyref.polymul(xs[0], ys[1], q), pyref.polymul(xs[1], ys[0], q))]
+            assert [L(r) for r in res] == [pyref.polymul(xs[0], ys[0], q), c1, pyref.polymul(xs[1], ys[1], q)]
+        out.append({"op": "ct_multiply", "n": n, "q": q, "ct1": L(x), "ct2": L(y), "out": L(res)})
+    for n, q, bl, lv in [(16, 97, 2, 4), (256, 7681, 4, 4), (1024, P27, 4, 7), (1024, P62, 16, 4)]:
+        t = oracle.NTT(n, q)
+        ct3 = oracle.testrandom_coeffs(23, q, 3 * n).reshape(3, n)
+        rlk = oracle.testrandom_coeffs(24, q, lv * 2 * n).reshape(lv, 2, n)
+        out.append({"op": "relinearize", "n": n, "q": q, "base_log": bl, "level": lv, "ct3": L(ct3), "rlk": L(rlk),
+                    "out": L(t.relinearize(bl, lv, ct3, rlk))})
+    for n, q, bl, lv, dim in [(32, 193, 3, 2, 6), (256, 7681, 4, 3, 8)]:
+        t = oracle.NTT(n, q)
+        bsk = oracle.testrandom_coeffs(25, q, dim * 2 * lv * 2 * n).reshape(dim, 2 * lv, 2, n)
+        lwe_a = oracle.testrandom_coeffs(26, q, dim)
+        lwe_a[0] = 0
+        acc = np.zeros((2, n), np.uint64)
+        acc[1] = oracle.testrandom_coeffs(27, q, n)
+        lwe_b = int(oracle.testrandom_coeffs(28, q, 1)[0])
+        got = t.blind_rotate(1, bl, lv, lwe_a, lwe_b, q, bsk, acc)
+        out.append({"op": "blind_rotate", "n": n, "q": q, "base_log": bl, "level": lv, "dim": dim, "bsk": L(bsk),
+                    "lwe_a": L(lwe_a), "lwe_b": lwe_b, "acc": L(acc), "out": L(got)})
+    return out
+
+
+GENERATORS = {
+    "reference_kat.json": reference_kat, "ntt_small.json": ntt_small, "ntt_large.json": ntt_large,
+    "modmul.json": modmul, "multi_limb.json": multi_limb, "extprod.json": extprod, "negacyclic.json": negacyclic,
+    "cipher.json": cipher,
+}
+
 if __name__ == "__main__":
-    dump("reference_kat.json", reference_kat())
-    dump("ntt_small.json", ntt_small())
-    dump("ntt_large.json", ntt_large())
-    dump("modmul.json", modmul())
-    dump("multi_limb.json", multi_limb())
-    dump("extprod.json", extprod())
-    dump("negacyclic.json", negacyclic())
+    # python make_golden.py [file.json ...]   (default: all)
+    for name in sys.argv[1:] or list(GENERATORS):
+        dump(name, GENERATORS[name]())

@@ -1,0 +1,263 @@
+"""GPU parity of the ciphertext-level ops:
+EncryptionEngine::multiply / relinearize / multiply_relin and the
+BootstrapEngine pieces (cmux, monomial rotation, blind_rotate,
+sample_extract, key_switch) -- HIP kernels through the C-ABI vs the CPU
+oracle's restatement (oracle/ref_cpu.c), bit-exact.
+
+Run on an MI355X with ``pytest -m gpu``.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+P27 = 132120577
+P62 = 4611686018326724609
+
+
+@pytest.fixture(scope="module")
+def fg():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import fhe_gpu
+
+    return fhe_gpu
+
+
+def rnd(seed, q, *shape):
+    return oracle.splitmix_fill(seed, q, int(np.prod(shape))).reshape(shape)
+
+
+# ------------------------------------------------------------ ciphertext multiply
+@pytest.mark.parametrize("n,q", [(4, 17), (16, 97), (256, 7681), (1024, P27), (2048, P62), (4096, P27),
+                                 (8192, P62), (16384, P27), (16384, P62)])
+def test_ct_multiply_vs_oracle(fg, n, q):
+    b = 3 if n >= 8192 else 5
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    eng = fg.EncryptionEngine(r)
+    x = rnd(n + 1, q, b, 2, n)
+    y = rnd(n + 2, q, b, 2, n)
+    got = eng.multiply(x, y)
+    assert got.shape == (b, 3, n)
+    for i in range(b):
+        assert (got[i] == t.ct_multiply(x[i], y[i])).all(), i
+    got_ntt = eng.multiply(x, y, is_ntt=True)
+    for i in range(b):
+        assert (got_ntt[i] == t.ct_multiply(x[i], y[i], is_ntt=True)).all(), i
+
+
+def test_ct_multiply_large_degree_and_raw_inputs(fg):
+    # n > 16384 takes the composed path; inputs are arbitrary u64 (x mod q)
+    for n, q in ((32768, P27), (1024, P62)):
+        r = fg.PolynomialRing(n, q)
+        t = oracle.NTT(n, q)
+        x = oracle.splitmix_fill(7, 0, 2 * 2 * n).reshape(2, 2, n)  # q = 0: raw 64-bit words
+        y = rnd(8, q, 2, 2, n)
+        got = fg.EncryptionEngine(r).multiply(x, y)
+        for i in range(2):
+            assert (got[i] == t.ct_multiply(x[i], y[i])).all(), (n, q, i)
+
+
+def test_ct_multiply_negacyclic_is_ring_tensor(fg):
+    n, q = 4096, P27
+    r = fg.PolynomialRing(n, q, mode="negacyclic")
+    x = rnd(11, q, 2, 2, n)
+    y = rnd(12, q, 2, 2, n)
+    got = fg.EncryptionEngine(r).multiply(x, y)
+    for i in range(2):
+        c0 = r.multiply(x[i, 0], y[i, 0])
+        c1 = r.add(r.multiply(x[i, 0], y[i, 1]), r.multiply(x[i, 1], y[i, 0]))
+        c2 = r.multiply(x[i, 1], y[i, 1])
+        assert (got[i, 0] == c0).all() and (got[i, 1] == c1).all() and (got[i, 2] == c2).all()
+
+
+@pytest.mark.parametrize("n,q,bl,lv", [(64, 257, 2, 4), (1024, P27, 4, 7), (1024, P27, 9, 3), (4096, P62, 16, 4),
+                                       (16384, P27, 4, 7), (16384, P62, 20, 3), (256, 7681, 63, 1)])
+def test_relinearize_vs_oracle(fg, n, q, bl, lv):
+    b = 2 if n >= 16384 else 4
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    ct3 = rnd(n * 3 + bl, q, b, 3, n)
+    ct3[0, 2, :5] = [0, q - 1, 2**63 + 5, 2**64 - 1, 1 << bl]  # raw c2 words decompose as given
+    rlk = rnd(lv * 13 + n, q, lv, 2, n)
+    ek = fg.EvaluationKey(r, rlk, bl)
+    eng = fg.EncryptionEngine(r)
+    got = eng.relinearize(ct3, ek)
+    assert got.shape == (b, 2, n)
+    for i in range(b):
+        assert (got[i] == t.relinearize(bl, lv, ct3[i], rlk)).all(), i
+
+
+def test_relinearize_without_keys_copies(fg):
+    n, q = 256, 7681
+    r = fg.PolynomialRing(n, q)
+    ct3 = oracle.splitmix_fill(3, 0, 2 * 3 * n).reshape(2, 3, n)
+    ek = fg.EvaluationKey(r, np.zeros((0, 2, n), np.uint64), 4)
+    got = fg.EncryptionEngine(r).relinearize(ct3, ek)
+    assert (got == ct3[:, :2]).all()
+
+
+@pytest.mark.parametrize("n,q", [(1024, P27), (16384, P27)])
+def test_multiply_relin_is_composition(fg, n, q):
+    r = fg.PolynomialRing(n, q)
+    eng = fg.EncryptionEngine(r)
+    x, y = rnd(21, q, 2, 2, n), rnd(22, q, 2, 2, n)
+    ek = fg.EvaluationKey(r, rnd(23, q, 7, 2, n), 4)
+    assert (eng.multiply_relin(x, y, ek) == eng.relinearize(eng.multiply(x, y), ek)).all()
+
+
+def test_ct_ops_device_tensors(fg):
+    import torch
+
+    n, q = 4096, P27
+    r = fg.PolynomialRing(n, q)
+    eng = fg.EncryptionEngine(r)
+    x, y = rnd(31, q, 4, 2, n), rnd(32, q, 4, 2, n)
+    rlk = rnd(33, q, 7, 2, n)
+    host = eng.multiply_relin(x, y, fg.EvaluationKey(r, rlk, 4))
+    dev = eng.multiply_relin(torch.from_numpy(x.view(np.int64)).cuda(), torch.from_numpy(y.view(np.int64)).cuda(),
+                             fg.EvaluationKey(r, torch.from_numpy(rlk.view(np.int64)).cuda(), 4))
+    torch.cuda.synchronize()
+    assert (dev.cpu().numpy().view(np.uint64) == host).all()
+
+
+# ------------------------------------------------------------ TFHE pieces
+@pytest.mark.parametrize("n,q,bl,lv", [(256, 7681, 4, 3), (1024, P62, 23, 1), (1024, P62, 15, 2),
+                                       (16384, P62, 15, 2)])
+def test_cmux_vs_oracle(fg, n, q, bl, lv):
+    k, b = 1, 2
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    ggsw = rnd(bl + n, q, (k + 1) * lv, k + 1, n)
+    ct0, ct1 = rnd(41, q, b, k + 1, n), rnd(42, q, b, k + 1, n)
+    got = be.cmux(be.prepare_ggsw(ggsw), ct0, ct1)
+    for i in range(b):
+        assert (got[i] == t.cmux(k, bl, lv, ggsw, ct0[i], ct1[i])).all(), i
+
+
+def test_glwe_rotate_vs_oracle(fg):
+    n, q, k = 1024, P27, 1
+    r = fg.PolynomialRing(n, q)
+    be = fg.BootstrapEngine(r, 4, 3, k)
+    rots = [0, 1, -1, n, -n, 2 * n - 1, 5 * n + 3, -(2**31)]
+    g = rnd(51, q, len(rots), k + 1, n)
+    g[0, 0, :3] = [2**64 - 1, q, q + 1]  # raw words: copied, or (q - x) % q when negated
+    got = be.multiply_glwe_by_monomial(g, rots)
+    for i, rot in enumerate(rots):
+        for j in range(k + 1):
+            assert (got[i, j] == oracle.rotate(q, g[i, j], rot)).all(), (rot, j)
+
+
+@pytest.mark.parametrize("n,q,bl,lv,dim", [(256, 7681, 4, 3, 12), (1024, P27, 9, 3, 10), (1024, P62, 23, 1, 16)])
+def test_blind_rotate_vs_oracle(fg, n, q, bl, lv, dim):
+    k, b = 1, 3
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(61, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a = rnd(62, q, b, dim)
+    lwe_a[0, 0] = 0          # rotation 0: the step is skipped
+    lwe_a[0, 1] = q - 1      # rotation 2N: computed (not skipped)
+    lwe_a[1, :] = 0          # whole ciphertext skipped
+    lwe_b = rnd(63, q, b)
+    acc0 = np.zeros((b, k + 1, n), np.uint64)
+    acc0[:, k] = rnd(64, q, b, n)   # (0, test polynomial)
+    acc0[2, k, :4] = [2**64 - 1, q, 0, 1]  # raw body words
+    acc = acc0.copy()
+    be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
+    for i in range(b):
+        exp = t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])
+        assert (acc[i] == exp).all(), i
+
+
+def test_sample_extract_vs_oracle(fg):
+    n, q, k = 1024, P27, 1
+    r = fg.PolynomialRing(n, q)
+    be = fg.BootstrapEngine(r, 4, 3, k)
+    g = rnd(71, q, 3, k + 1, n)
+    g[1, 0, 5] = 2**64 - 1
+    a, b = be.sample_extract(g)
+    for i in range(3):
+        ea, eb = oracle.sample_extract(q, g[i])
+        assert (a[i] == ea).all() and int(b[i]) == eb
+
+
+@pytest.mark.parametrize("q,bl,lv", [(P27, 4, 3), (P27, 2, 8), (P62, 7, 4), ((1 << 61) + 1, 10, 6)])
+def test_key_switch_vs_oracle(fg, q, bl, lv):
+    in_dim, out_dim, b = 96, 70, 37
+    ksk_a = rnd(81, q, in_dim * lv, out_dim)
+    ksk_b = rnd(82, q, in_dim * lv)
+    lwe_a = rnd(83, q, b, in_dim)
+    lwe_b = rnd(84, q, b)
+    lwe_a[0, :] = 0                  # no digit: body returned raw
+    lwe_b[0] = 2**64 - 3
+    lwe_b[1] = 2**64 - 2             # b + q wraps in the first update
+    lwe_a[2, :] = 1 << (bl * lv - 1) if bl * lv < 64 else 1
+    oa, ob = fg.BootstrapEngine.key_switch(q, bl, lv, ksk_a, ksk_b, lwe_a, lwe_b)
+    for i in range(b):
+        ea, eb = oracle.key_switch(q, bl, lv, ksk_a, ksk_b, lwe_a[i], int(lwe_b[i]))
+        assert (oa[i] == ea).all(), i
+        assert int(ob[i]) == eb, i
+
+
+def test_bootstrap_pipeline_device(fg):
+    """blind_rotate -> sample_extract -> key_switch on device tensors equals
+    the oracle's bootstrap_with_test_poly sequence (:679-708)."""
+    import torch
+
+    n, q, bl, lv, dim, k, b = 512, 12289, 4, 3, 8, 1, 4
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(91, q, dim, (k + 1) * lv, k + 1, n)
+    lwe_a, lwe_b = rnd(92, q, b, dim), rnd(93, q, b)
+    test_poly = rnd(94, q, n)
+    ksk_a, ksk_b = rnd(95, q, k * n * 2, dim), rnd(96, q, k * n * 2)
+
+    def T(x):
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
+
+    acc = torch.zeros((b, k + 1, n), dtype=torch.int64, device="cuda")
+    acc[:, k] = T(test_poly)
+    be.blind_rotate(acc, T(lwe_a), T(lwe_b), be.prepare_ggsw(T(bsk)))
+    ea, eb = be.sample_extract(acc)
+    oa, ob = fg.BootstrapEngine.key_switch(q, 7, 2, T(ksk_a), T(ksk_b), ea, eb)
+    torch.cuda.synchronize()
+    oa, ob = oa.cpu().numpy().view(np.uint64), ob.cpu().numpy().view(np.uint64)
+    for i in range(b):
+        a0 = np.zeros((k + 1, n), np.uint64)
+        a0[k] = test_poly
+        accx = t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, a0)
+        xa, xb = oracle.sample_extract(q, accx)
+        ka, kb = oracle.key_switch(q, 7, 2, ksk_a, ksk_b, xa, xb)
+        assert (oa[i] == ka).all() and int(ob[i]) == kb, i
+
+
+def test_cipher_golden_gpu(fg, golden_dir):
+    import json
+    import os
+
+    with open(os.path.join(golden_dir, "cipher.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        n, q = c["n"], c["q"]
+        r = fg.PolynomialRing(n, q)
+        U = lambda x, *s: np.array(x, np.uint64).reshape(s)  # noqa: E731
+        if c["op"] == "ct_multiply":
+            got = fg.EncryptionEngine(r).multiply(U(c["ct1"], 1, 2, n), U(c["ct2"], 1, 2, n))
+        elif c["op"] == "relinearize":
+            ek = fg.EvaluationKey(r, U(c["rlk"], c["level"], 2, n), c["base_log"])
+            got = fg.EncryptionEngine(r).relinearize(U(c["ct3"], 1, 3, n), ek)
+        else:
+            be = fg.BootstrapEngine(r, c["base_log"], c["level"], 1)
+            got = U(c["acc"], 1, 2, n).copy()
+            be.blind_rotate(got, U(c["lwe_a"], 1, c["dim"]), U([c["lwe_b"]], 1),
+                            be.prepare_ggsw(U(c["bsk"], c["dim"], 2 * c["level"], 2, n)))
+        assert [int(v) for v in got.ravel()] == c["out"], (c["op"], n, q)
