@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--only", default="", help="run only this kernel (fwd_mul|polymul|fwd|inv) for profiling")
     ap.add_argument("--no-check", action="store_true", help="skip the oracle spot check (profiling runs)")
+    ap.add_argument("--no-cipher", dest="cipher", action="store_false",
+                    help="skip the ciphertext-level side metrics (ct multiply, relinearize, blind rotate)")
     return ap.parse_args()
 
 
@@ -151,6 +153,56 @@ def _spot_check(ring, a, b, out, n, q, batch):
         return f"unchecked: {e}"
 
 
+def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
+    """Ciphertext-level ops: BFV-style multiply and
+    relinearisation at N=16384, TFHE blind rotation at N=1024.  Reported
+    beside the headline metric, never as `value`."""
+    res = {}
+    dev = torch.cuda.current_device()
+    g = torch.Generator(device="cuda").manual_seed(77)
+    if only in ("", "ct_mul", "relin"):
+        n, q, B, bl, lv = 16384, P27, 8192, 4, 7
+        ring = fhe_gpu.PolynomialRing(n, q, device=dev)
+        eng = fhe_gpu.EncryptionEngine(ring)
+        x = torch.randint(0, q, (B, 2, n), device="cuda", dtype=torch.int64, generator=g)
+        y = torch.randint(0, q, (B, 2, n), device="cuda", dtype=torch.int64, generator=g)
+        ct3 = torch.empty((B, 3, n), device="cuda", dtype=torch.int64)
+        if only in ("", "ct_mul"):
+            wall, kms = timed(dist, lambda: eng.multiply(x, y, out=ct3), steps, warmup)
+            res["ct_multiply"] = {"n": n, "q": q, "batch": B, "per_s": B * steps / wall, "kernel_ms": kms,
+                                  "transforms_per_unit": 7, "bytes_per_unit": 56 * n,
+                                  "achieved_GBs": 56 * n * B / (kms * 1e-3) / 1e9}
+        if only in ("", "relin"):
+            ek = fhe_gpu.EvaluationKey(ring, torch.randint(0, q, (lv, 2, n), device="cuda", dtype=torch.int64,
+                                                           generator=g), bl)
+            out = torch.empty((B, 2, n), device="cuda", dtype=torch.int64)
+            eng.multiply(x, y, out=ct3)
+            wall, kms = timed(dist, lambda: eng.relinearize(ct3, ek, out=out), steps, warmup)
+            res["relinearize"] = {"n": n, "q": q, "batch": B, "base_log": bl, "level": lv, "per_s": B * steps / wall,
+                                  "kernel_ms": kms, "transforms_per_unit": lv + 2, "bytes_per_unit": 40 * n,
+                                  "achieved_GBs": 40 * n * B / (kms * 1e-3) / 1e9}
+            del out, ek
+        del x, y, ct3
+    if only in ("", "blind_rotate"):
+        # tfhe-128-fast shape (parameter_set.cpp): N=1024, k=1, B=23, L=1, n=742;
+        # q = the 62-bit prime (Q_40_1 = 2^40+1 is not prime, SURVEY.md a18)
+        n, q, bl, lv, dim, B = 1024, P62, 23, 1, 742, 8192
+        ring = fhe_gpu.PolynomialRing(n, q, device=dev)
+        be = fhe_gpu.BootstrapEngine(ring, bl, lv, 1)
+        bsk = be.prepare_ggsw(torch.randint(0, q, (dim, 2 * lv, 2, n), device="cuda", dtype=torch.int64, generator=g))
+        lwe_a = torch.randint(0, q, (B, dim), device="cuda", dtype=torch.int64, generator=g)
+        lwe_b = torch.randint(0, q, (B,), device="cuda", dtype=torch.int64, generator=g)
+        acc = torch.zeros((B, 2, n), device="cuda", dtype=torch.int64)
+        st = max(1, steps // 4)
+        wall, kms = timed(dist, lambda: be.blind_rotate(acc, lwe_a, lwe_b, bsk), st, 1)
+        res["blind_rotate"] = {"n": n, "q": q, "k": 1, "base_log": bl, "level": lv, "lwe_dim": dim, "batch": B,
+                               "per_s": B * st / wall, "ms_per_batch": kms,
+                               "cmux_per_s": B * dim * st / wall}
+        del bsk, lwe_a, lwe_b, acc
+    torch.cuda.empty_cache()
+    return res
+
+
 def pmc_traffic(kernel, n, batch, q):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of the
     same workload (profiles/*/summary.json, tools/summarize_profile.py)."""
@@ -201,8 +253,13 @@ def main():
     import fhe_gpu
 
     n, B, K, W = args.n, args.batch, args.steps, args.warmup
-    r = gpu_workload(fhe_gpu, n, args.q, B, K, W, dist, args.only, check=not args.no_check)
     extra = {}
+    if args.only in ("ct_mul", "relin", "blind_rotate"):  # profiling runs of the side metrics
+        c = cipher_workload(fhe_gpu, K, W, dist, args.only)
+        if rank == 0:
+            print(json.dumps({"cipher": c}), flush=True)
+        return
+    r = gpu_workload(fhe_gpu, n, args.q, B, K, W, dist, args.only, check=not args.no_check)
     if args.q62 and not args.only:
         r62 = gpu_workload(fhe_gpu, n, P62, B, max(3, K // 4), 1, dist)
         extra["q62"] = {
@@ -212,6 +269,8 @@ def main():
             "fwd_mul_kernel_ms": r62["fwd_mul"][1], "polymul_kernel_ms": r62["polymul"][1],
             "parity_ok": r62["parity_ok"],
         }
+    if args.cipher and not args.only:
+        extra["cipher"] = cipher_workload(fhe_gpu, max(3, K // 4), 1, dist)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
