@@ -58,18 +58,25 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     const uint64_t *xr = x + poly * 2 * G::N, *yr = y + poly * 2 * G::N;
     uint64_t *orow = out + poly * 3 * G::N;
     W creg[NL == 0 ? G::E : 1];
+    // HBM slots (NL < 3) hold W words in the first half of their u64 row
+    auto hrow = [&](int s) -> W * { return reinterpret_cast<W *>(orow + (size_t)(s + 1) * G::N); };
     // slot s at global index gi (own positions only)
     auto ld = [&](int s, uint32_t gi, int e) -> W {
         if (NL == 3 || (NL == 1 && s == 2)) return lds_all[G::P * G::LW + ((NL == 3 ? s : 0) * G::P + pl) * G::N + gi];
         if (s == 2) return creg[NL == 0 ? e : 0];
-        return valid ? (W)orow[(size_t)(s + 1) * G::N + gi] : W(0);
+        return valid ? hrow(s)[gi] : W(0);
     };
     auto st = [&](int s, uint32_t gi, int e, W val) {
         if (NL == 3 || (NL == 1 && s == 2)) lds_all[G::P * G::LW + ((NL == 3 ? s : 0) * G::P + pl) * G::N + gi] = val;
         else if (s == 2) creg[NL == 0 ? e : 0] = val;
-        else if (valid) orow[(size_t)(s + 1) * G::N + gi] = (uint64_t)val;
+        else if (valid) hrow(s)[gi] = val;
     };
     constexpr int SA = 0, SB = 1, SC = 2;
+    // HBM slots A/B are prefetched into registers during the last pass of
+    // the transform that consumes them (their latency overlaps it; with one
+    // workgroup per CU nothing else would hide it).
+    constexpr bool HB = NL == 1;  // NL == 0 (C in VGPRs) has no registers to spare
+    W pre[2][HB ? G::E : 1];
     W v[G::E];
     // a fresh opaque copy of the lane index per phase: stops the compiler
     // from keeping one phase's address arithmetic live across the next
@@ -79,9 +86,20 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
         asm volatile("" : "+v"(t));
         return t;
     };
+    uint32_t tp = 0;
+    auto fetch = [&](int s, int k) {
+        if constexpr (HB) {
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) pre[k][e] = ld(s, gidx<LOGN, G::NP - 1>(tp, e), e);
+        }
+    };
+    auto slot = [&](int s, int k, uint32_t gi, int e) -> W {
+        if constexpr (HB) return pre[k][e];
+        else return ld(s, gi, e);
+    };
 
     // 1. A = X0
-    uint32_t tp = lane();
+    tp = lane();
     fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) st(SA, gidx<LOGN, G::NP - 1>(tp, e), e, fwd_to_canon<LAZY>(v[e], A));
@@ -89,13 +107,13 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 
     // 2. Y0: B = Y0, c0 = inv(X0 Y0)
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr, valid, A);
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr, valid, A, 0, 0, [&] { fetch(SA, 0); });
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
         const W y0 = v[e];
         st(SB, gi, e, fwd_to_canon<LAZY>(y0, A));
-        v[e] = A.ar.mont(ld(SA, gi, e), y0);
+        v[e] = A.ar.mont(slot(SA, 0, gi, e), y0);
     }
     __syncthreads();
     tp = lane();
@@ -104,25 +122,28 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 
     // 3. X1: C = X1 Y0, B = X1
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr + G::N, valid, A);
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr + G::N, valid, A, 0, 0, [&] { fetch(SB, 1); });
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
         const W x1 = v[e];
-        st(SC, gi, e, A.ar.mont(ld(SB, gi, e), x1));
+        st(SC, gi, e, A.ar.mont(slot(SB, 1, gi, e), x1));
         st(SB, gi, e, fwd_to_canon<LAZY>(x1, A));
     }
     if constexpr (G::NP > 1) __syncthreads();
 
     // 4. Y1: c1 = C + X0 Y1, C = X1 Y1
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr + G::N, valid, A);
+    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr + G::N, valid, A, 0, 0, [&] {
+        fetch(SA, 0);
+        fetch(SB, 1);
+    });
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
         const W y1 = v[e];
-        const W c1 = A.ar.red2q(ld(SC, gi, e) + A.ar.mont(ld(SA, gi, e), y1));
-        st(SC, gi, e, A.ar.mont(ld(SB, gi, e), y1));
+        const W c1 = A.ar.red2q(ld(SC, gi, e) + A.ar.mont(slot(SA, 0, gi, e), y1));
+        st(SC, gi, e, A.ar.mont(slot(SB, 1, gi, e), y1));
         v[e] = c1;
     }
     __syncthreads();  // every slot read of rows 1/2 precedes their final stores

@@ -33,6 +33,12 @@ for q in [int(x) for x in args.qs.split(",")]:
     for bl, lv in ((23, 1), (15, 2)):
         ggsw = torch.randint(0, q, (2 * lv, 2, n), device="cuda", dtype=torch.int64, generator=g)
         eps[lv] = fhe_gpu.ExternalProduct(ring, ggsw, bl, lv)
+    eng = fhe_gpu.EncryptionEngine(ring)
+    nct = B // 4  # ciphertexts for ct_mul / relin
+    cx, cy = a[: 2 * nct].view(nct, 2, n), b[: 2 * nct].view(nct, 2, n)
+    c3 = out[: 3 * nct].view(nct, 3, n)
+    c2 = a[2 * nct: 4 * nct].view(nct, 2, n)
+    ek = fhe_gpu.EvaluationKey(ring, torch.randint(0, q, (7, 2, n), device="cuda", dtype=torch.int64, generator=g), 4)
     glwe = a[: B // 2].view(B // 4, 2, n)  # B/4 ciphertexts (k = 1)
     gout = out[: B // 2].view(B // 4, 2, n)
     for op in args.ops.split(","):
@@ -41,7 +47,9 @@ for q in [int(x) for x in args.qs.split(",")]:
               "fwd": lambda: ring.forward_ntt(a, out=out),
               "inv": lambda: ring.inverse_ntt(a, out=out),
               "ext1": lambda: eps[1](glwe, out=gout),
-              "ext2": lambda: eps[2](glwe, out=gout)}[op]
+              "ext2": lambda: eps[2](glwe, out=gout),
+              "ct_mul": lambda: eng.multiply(cx, cy, out=c3),
+              "relin": lambda: eng.relinearize(c3, ek, out=c2)}[op]
         fn()
         torch.cuda.synchronize()
         chk = int(out[:8].sum().item()) ^ int(out[-8:].sum().item())
