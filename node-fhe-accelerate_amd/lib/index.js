@@ -37,6 +37,22 @@ class PolynomialEngine {
   externalProduct(glwe, ggsw, baseLog, level, out = new BigUint64Array(glwe.length)) {
     return this.ctx.externalProduct(glwe, ggsw, baseLog, level, out);
   }
+  /** EncryptionEngine::multiply: ct [batch][2][n] -> [batch][3][n] */
+  ctMultiply(ct1, ct2, { isNtt = false } = {}, out = new BigUint64Array(ct1.length / 2 * 3)) {
+    return this.ctx.ctMultiply(ct1, ct2, out, isNtt ? 1 : 0);
+  }
+  /** EncryptionEngine::relinearize: ct3 [batch][3][n], rlk [level][2][n] (a_l, b_l) */
+  relinearize(ct3, rlk, baseLog = 4, out = new BigUint64Array(ct3.length / 3 * 2)) {
+    return this.ctx.relinearize(ct3, rlk, baseLog, out);
+  }
+  /** EncryptionEngine::multiply_relin */
+  multiplyRelin(ct1, ct2, rlk, baseLog = 4) {
+    return this.relinearize(this.ctMultiply(ct1, ct2), rlk, baseLog);
+  }
+  /** BootstrapEngine::blind_rotate (k = 1), in place on acc [batch][2][n] */
+  blindRotate(acc, lweA, lweB, bsk, baseLog, level) {
+    return this.ctx.blindRotate(acc, lweA, lweB, bsk, baseLog, level);
+  }
   info() { return this.ctx.info(); }
 }
 

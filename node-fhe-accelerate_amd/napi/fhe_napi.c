@@ -422,6 +422,97 @@ static napi_value ctx_ext_product(napi_env env, napi_callback_info info) {
     return argv[4];
 }
 
+/* ctMultiply(ct1, ct2, out, isNtt?): ct [batch][2][n] -> out [batch][3][n]
+ * (EncryptionEngine::multiply, encryption.cpp:737-798) */
+static napi_value ctx_ct_multiply(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    fhe_ctx *c = ctx_this(env, info, &argc, argv);
+    uint64_t *x, *y, *o, is_ntt = 0;
+    size_t nx, ny, no;
+    int neg;
+    if (!c || argc < 3 || get_u64_array(env, argv[0], &x, &nx) || get_u64_array(env, argv[1], &y, &ny) ||
+        get_u64_array(env, argv[2], &o, &no) || nx != ny ||
+        (argc > 3 && (get_u64(env, argv[3], &is_ntt, &neg) || neg))) {
+        napi_throw_type_error(env, "INVALID_PARAMETERS", "ctMultiply(ct1, ct2, out, isNtt?)");
+        return NULL;
+    }
+    fhe_ctx_info ci;
+    fhe_ctx_get_info(c, &ci);
+    const size_t per = 2 * (size_t)ci.n;
+    if (nx % per || no != nx / 2 * 3) {
+        napi_throw_range_error(env, "INVALID_PARAMETERS", "ciphertexts must be [batch][2][n], out [batch][3][n]");
+        return NULL;
+    }
+    int rc = fhe_ct_multiply_batch(c, x, y, o, nx / per, (int)is_ntt, FHE_HOST);
+    if (rc) return throw_fhe(env, rc);
+    return argv[2];
+}
+
+/* relinearize(ct3, rlk, baseLog, out): rlk [level][2][n] (a_l, b_l) in
+ * coefficient form (KeySwitchKey), out [batch][2][n]
+ * (EncryptionEngine::relinearize, encryption.cpp:904-980) */
+static napi_value ctx_relinearize(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    fhe_ctx *c = ctx_this(env, info, &argc, argv);
+    uint64_t *ct, *k, *o, bl;
+    size_t nc, nk, no;
+    int neg;
+    if (!c || argc < 4 || get_u64_array(env, argv[0], &ct, &nc) || get_u64_array(env, argv[1], &k, &nk) ||
+        get_u64(env, argv[2], &bl, &neg) || neg || get_u64_array(env, argv[3], &o, &no)) {
+        napi_throw_type_error(env, "INVALID_PARAMETERS", "relinearize(ct3, rlk, baseLog, out)");
+        return NULL;
+    }
+    fhe_ctx_info ci;
+    fhe_ctx_get_info(c, &ci);
+    const size_t n = ci.n;
+    if (nc % (3 * n) || nk % (2 * n) || no != nc / 3 * 2) {
+        napi_throw_range_error(env, "INVALID_PARAMETERS", "ct3 [batch][3][n], rlk [level][2][n], out [batch][2][n]");
+        return NULL;
+    }
+    const uint32_t level = (uint32_t)(nk / (2 * n));
+    uint64_t *prep = level ? (uint64_t *)malloc(nk * 8) : NULL;
+    int rc = level ? fhe_relin_key_prepare(c, level, k, prep, FHE_HOST) : 0;
+    if (!rc) rc = fhe_relinearize_batch(c, bl ? (uint32_t)bl : 4, level, ct, prep, o, nc / (3 * n), FHE_HOST);
+    free(prep);
+    if (rc) return throw_fhe(env, rc);
+    return argv[3];
+}
+
+/* blindRotate(acc, lweA, lweB, bsk, baseLog, level): k = 1, in place on acc
+ * [batch][2][n]; lweA [batch][dim]; lweB [batch]; bsk [dim][2*level][2][n]
+ * coefficient-form GGSWs (BootstrapEngine::blind_rotate :547-577) */
+static napi_value ctx_blind_rotate(napi_env env, napi_callback_info info) {
+    size_t argc = 6;
+    napi_value argv[6];
+    fhe_ctx *c = ctx_this(env, info, &argc, argv);
+    uint64_t *acc, *la, *lb, *bsk, bl, lv;
+    size_t nacc, nla, nlb, nbsk;
+    int neg;
+    if (!c || argc < 6 || get_u64_array(env, argv[0], &acc, &nacc) || get_u64_array(env, argv[1], &la, &nla) ||
+        get_u64_array(env, argv[2], &lb, &nlb) || get_u64_array(env, argv[3], &bsk, &nbsk) ||
+        get_u64(env, argv[4], &bl, &neg) || neg || get_u64(env, argv[5], &lv, &neg) || neg || lv == 0) {
+        napi_throw_type_error(env, "INVALID_PARAMETERS", "blindRotate(acc, lweA, lweB, bsk, baseLog, level)");
+        return NULL;
+    }
+    fhe_ctx_info ci;
+    fhe_ctx_get_info(c, &ci);
+    const size_t n = ci.n, ggsw = 4 * lv * n;
+    if (nacc % (2 * n) || nlb != nacc / (2 * n) || (nlb && nla % nlb) || nbsk % ggsw ||
+        (nlb && nbsk / ggsw != nla / nlb)) {
+        napi_throw_range_error(env, "INVALID_PARAMETERS", "shape mismatch (k = 1)");
+        return NULL;
+    }
+    const uint32_t dim = nlb ? (uint32_t)(nla / nlb) : 0;
+    uint64_t *prep = (uint64_t *)malloc(nbsk ? nbsk * 8 : 8);
+    int rc = nbsk ? fhe_ggsw_prepare(c, 1, (uint32_t)(lv * dim), bsk, prep, FHE_HOST) : 0;
+    if (!rc) rc = fhe_blind_rotate_batch(c, 1, (uint32_t)bl, (uint32_t)lv, dim, la, lb, ci.q, prep, acc, nlb, FHE_HOST);
+    free(prep);
+    if (rc) return throw_fhe(env, rc);
+    return argv[0];
+}
+
 static napi_value ctx_info(napi_env env, napi_callback_info info) {
     size_t argc = 0;
     fhe_ctx *c = ctx_this(env, info, &argc, NULL);
@@ -480,6 +571,9 @@ static napi_value init(napi_env env, napi_value exports) {
         {"mulScalar", NULL, ctx_mul_scalar, NULL, NULL, NULL, napi_default, NULL},
         {"forwardMul", NULL, ctx_fwd_mul, NULL, NULL, NULL, napi_default, NULL},
         {"externalProduct", NULL, ctx_ext_product, NULL, NULL, NULL, napi_default, NULL},
+        {"ctMultiply", NULL, ctx_ct_multiply, NULL, NULL, NULL, napi_default, NULL},
+        {"relinearize", NULL, ctx_relinearize, NULL, NULL, NULL, napi_default, NULL},
+        {"blindRotate", NULL, ctx_blind_rotate, NULL, NULL, NULL, napi_default, NULL},
         {"info", NULL, ctx_info, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_value ctx_cls;

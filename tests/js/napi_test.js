@@ -101,6 +101,19 @@ if (mode === 'cpu') {
       assert.deepStrictEqual(Array.from(out), c.out.map(BigInt));
     }
   });
+  test('ciphertext multiply / relinearize / blind rotate vs golden', () => {
+    for (const c of goldenBig('cipher.json')) {
+      const e = new fhe.PolynomialEngine(c.n, BigInt(c.q));
+      let got;
+      if (c.op === 'ct_multiply') got = e.ctMultiply(U(c.ct1), U(c.ct2));
+      else if (c.op === 'relinearize') got = e.relinearize(U(c.ct3), U(c.rlk), c.base_log);
+      else {
+        got = U(c.acc);
+        e.blindRotate(got, U(c.lwe_a), U([c.lwe_b]), U(c.bsk), c.base_log, c.level);
+      }
+      assert.deepStrictEqual(Array.from(got), c.out.map(BigInt), `${c.op} n=${c.n}`);
+    }
+  });
   test('negacyclic mode is the ring product', () => {
     for (const c of goldenBig('negacyclic.json')) {
       const e = new fhe.PolynomialEngine(c.n, BigInt(c.q), { mode: 'negacyclic' });
