@@ -143,6 +143,25 @@ int fhe_external_product_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint
 int fhe_decompose_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const uint64_t *poly, uint64_t *out,
                         size_t npoly, int where);
 
+/* ---- RNS multi-modulus ring (PolynomialRing(degree, moduli),
+ * polynomial_ring.cpp:224-237): one transform context per modulus, all on
+ * one stream.  RNS polynomials are modulus-major: [count][batch][n] (limb i
+ * of every polynomial contiguous), so each limb is one launch over a
+ * contiguous batch.  The reference's ring operations use moduli_[0] only;
+ * these apply the operation to every limb. */
+typedef struct fhe_rns_ctx fhe_rns_ctx;
+int fhe_rns_ctx_create(uint32_t n, const uint64_t *moduli, uint32_t count, int mode, int device, fhe_rns_ctx **out);
+void fhe_rns_ctx_destroy(fhe_rns_ctx *rns);
+int fhe_rns_ctx_limb(const fhe_rns_ctx *rns, uint32_t i, fhe_ctx **out);
+int fhe_rns_ntt_fwd_batch(fhe_rns_ctx *rns, const uint64_t *in, uint64_t *out, size_t batch, int where);
+int fhe_rns_ntt_inv_batch(fhe_rns_ctx *rns, const uint64_t *in, uint64_t *out, size_t batch, int where);
+int fhe_rns_polymul_batch(fhe_rns_ctx *rns, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch,
+                          int where);
+int fhe_rns_pointwise_batch(fhe_rns_ctx *rns, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch,
+                            int where);
+int fhe_rns_add_batch(fhe_rns_ctx *rns, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch, int where);
+int fhe_rns_sub_batch(fhe_rns_ctx *rns, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch, int where);
+
 /* ---- BFV-style ciphertext multiplication (encryption.cpp:737-980) -------
  * A ciphertext is its component polynomials, contiguous: ct [batch][2][n]
  * (c0, c1); a degree-2 product [batch][3][n] (c0, c1, c2).

@@ -696,6 +696,74 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, c
     return rc;
 }
 
+// ---------------------------------------------------------------- RNS ring
+struct fhe_rns_ctx {
+    std::vector<fhe_ctx *> limbs;
+};
+
+int fhe_rns_ctx_create(uint32_t n, const uint64_t *moduli, uint32_t count, int mode, int device, fhe_rns_ctx **out) {
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    // PolynomialRing(degree, moduli) (polynomial_ring.cpp:228-230)
+    if (count == 0 || !moduli) return fail(FHE_ERR_INVALID_ARG, "At least one modulus required");
+    fhe_rns_ctx *r = new fhe_rns_ctx();
+    for (uint32_t i = 0; i < count; ++i) {
+        fhe_ctx *c = nullptr;
+        const int rc = fhe_ctx_create(n, moduli[i], mode, device, &c);
+        if (rc != FHE_OK) {
+            const std::string msg = g_err;
+            fhe_rns_ctx_destroy(r);
+            return fail(rc, msg);
+        }
+        if (!r->limbs.empty()) fhe_ctx_set_stream(c, r->limbs[0]->stream);  // one stream: limbs run in order
+        r->limbs.push_back(c);
+    }
+    *out = r;
+    return FHE_OK;
+}
+
+void fhe_rns_ctx_destroy(fhe_rns_ctx *r) {
+    if (!r) return;
+    for (auto it = r->limbs.rbegin(); it != r->limbs.rend(); ++it) fhe_ctx_destroy(*it);
+    delete r;
+}
+
+int fhe_rns_ctx_limb(const fhe_rns_ctx *r, uint32_t i, fhe_ctx **out) {
+    if (!r || !out) return fail(FHE_ERR_INVALID_ARG, "null argument");
+    if (i >= r->limbs.size()) return fail(FHE_ERR_INVALID_ARG, "limb index out of range");
+    *out = r->limbs[i];
+    return FHE_OK;
+}
+
+extern "C++" {
+template <typename F>
+static int rns_each(fhe_rns_ctx *r, size_t batch, F &&fn) {
+    if (!r) return fail(FHE_ERR_INVALID_ARG, "null context");
+    for (size_t i = 0; i < r->limbs.size(); ++i)
+        if (int rc = fn(r->limbs[i], i * batch * r->limbs[i]->n)) return rc;
+    return FHE_OK;
+}
+}
+#define RNS_UNARY(NAME, FN)                                                                              \
+    int NAME(fhe_rns_ctx *r, const uint64_t *in, uint64_t *out, size_t batch, int where) {              \
+        if (batch && (!in || !out)) return fail(FHE_ERR_INVALID_ARG, "null buffer");                     \
+        return rns_each(r, batch, [&](fhe_ctx *c, size_t off) { return FN(c, in + off, out + off, batch, where); }); \
+    }
+#define RNS_BINARY(NAME, FN)                                                                             \
+    int NAME(fhe_rns_ctx *r, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) { \
+        if (batch && (!a || !b || !out)) return fail(FHE_ERR_INVALID_ARG, "null buffer");                \
+        return rns_each(r, batch,                                                                        \
+                        [&](fhe_ctx *c, size_t off) { return FN(c, a + off, b + off, out + off, batch, where); }); \
+    }
+RNS_UNARY(fhe_rns_ntt_fwd_batch, fhe_ntt_fwd_batch)
+RNS_UNARY(fhe_rns_ntt_inv_batch, fhe_ntt_inv_batch)
+RNS_BINARY(fhe_rns_polymul_batch, fhe_polymul_batch)
+RNS_BINARY(fhe_rns_pointwise_batch, fhe_pointwise_batch)
+RNS_BINARY(fhe_rns_add_batch, fhe_poly_add_batch)
+RNS_BINARY(fhe_rns_sub_batch, fhe_poly_sub_batch)
+#undef RNS_UNARY
+#undef RNS_BINARY
+
 static int check_tfhe(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level) {
     FHE_TRY(check_fused(c, "external product"));
     if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");

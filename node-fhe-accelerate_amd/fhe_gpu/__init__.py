@@ -9,6 +9,7 @@ reference (cpp/include/...)    here
 =============================  ==============================================
 NTTProcessor                   :class:`NTTProcessor`   (ntt_processor.h:49-306)
 PolynomialRing                 :class:`PolynomialRing` (polynomial_ring.h:101-516)
+PolynomialRing(degree, moduli) :class:`RNSPolynomialRing` (polynomial_ring.cpp:224-237)
 ModularArithmetic              :class:`ModularArithmetic` (modular_arithmetic.h:20-80;
                                the N-API class of index.d.ts:32-44)
 BarrettReducer                 :class:`BarrettReducer` (modular_arithmetic.h:82-)
@@ -111,6 +112,15 @@ SIGNATURES = [
     ("fhe_external_product_batch", C.c_int,
      [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
     ("fhe_decompose_batch", C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_rns_ctx_create", C.c_int, [C.c_uint32, u64p, C.c_uint32, C.c_int, C.c_int, C.POINTER(vp)]),
+    ("fhe_rns_ctx_destroy", None, [vp]),
+    ("fhe_rns_ctx_limb", C.c_int, [vp, C.c_uint32, C.POINTER(vp)]),
+    ("fhe_rns_ntt_fwd_batch", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_rns_ntt_inv_batch", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_rns_polymul_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_rns_pointwise_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_rns_add_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_rns_sub_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int]),
     ("fhe_ct_multiply_batch", C.c_int, [vp, vp, vp, vp, C.c_size_t, C.c_int, C.c_int]),
     ("fhe_relin_key_prepare", C.c_int, [vp, C.c_uint32, vp, vp, C.c_int]),
     ("fhe_relinearize_batch", C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
@@ -422,6 +432,88 @@ class PolynomialRing(NTTProcessor):
 
     def from_ntt(self, p, out=None):
         return self.inverse_ntt(p, out)
+
+
+class RNSPolynomialRing:
+    """PolynomialRing(degree, moduli) (polynomial_ring.cpp:224-237): one
+    transform context per modulus on one stream.  Arrays are modulus-major
+    [len(moduli), ..., n]; every operation applies to every limb (the
+    reference's ring operations use moduli_[0] only)."""
+
+    def __init__(self, degree: int, moduli, mode: str = "compat", device: int = 0):
+        m = {"compat": MODE_COMPAT, "negacyclic": MODE_NEGACYCLIC}.get(mode)
+        if m is None:
+            raise FHEError(-9, f"unknown mode {mode!r}")
+        mods = [int(x) for x in moduli]
+        arr = (C.c_uint64 * max(1, len(mods)))(*mods)
+        h = C.c_void_p()
+        _check(lib().fhe_rns_ctx_create(degree, arr, len(mods), m, device, C.byref(h)))
+        self._h = h
+        self.degree, self.moduli, self.mode, self.device = degree, mods, mode, device
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.fhe_rns_ctx_destroy(h)
+        self._h = None
+
+    __del__ = close
+
+    def _batch(self, x) -> int:
+        shape = tuple(x.shape)
+        if len(shape) < 2 or shape[0] != len(self.moduli) or shape[-1] != self.degree:
+            raise FHEError(-5, f"RNS arrays must be [{len(self.moduli)}, ..., {self.degree}]")
+        return int(np.prod(shape[1:-1])) if len(shape) > 2 else 1
+
+    def _bind(self, where):
+        if where == FHE_DEVICE:
+            first = C.c_void_p()
+            _check(lib().fhe_rns_ctx_limb(self._h, 0, C.byref(first)))
+            _check(lib().fhe_ctx_set_stream(first, _stream_ptr()))
+            for i in range(1, len(self.moduli)):
+                c = C.c_void_p()
+                _check(lib().fhe_rns_ctx_limb(self._h, i, C.byref(c)))
+                _check(lib().fhe_ctx_set_stream(c, _stream_ptr()))
+
+    def _unary(self, fn, x, out):
+        x = _as_u64(x)
+        nb = self._batch(x)
+        out = _like(x) if out is None else out
+        bi, bo = _Buf(x), _Buf(out, True)
+        w = _where(bi, bo)
+        self._bind(w)
+        _check(fn(self._h, bi.ptr, bo.ptr, nb, w))
+        return out
+
+    def _binary(self, fn, a, b, out):
+        a, b = _as_u64(a), _as_u64(b)
+        nb = self._batch(a)
+        if tuple(b.shape) != tuple(a.shape):
+            raise FHEError(-9, "operand shapes differ")
+        out = _like(a) if out is None else out
+        ba, bb, bo = _Buf(a), _Buf(b), _Buf(out, True)
+        w = _where(ba, bb, bo)
+        self._bind(w)
+        _check(fn(self._h, ba.ptr, bb.ptr, bo.ptr, nb, w))
+        return out
+
+    def forward_ntt(self, x, out=None):
+        return self._unary(lib().fhe_rns_ntt_fwd_batch, x, out)
+
+    def inverse_ntt(self, x, out=None):
+        return self._unary(lib().fhe_rns_ntt_inv_batch, x, out)
+
+    def multiply(self, a, b, out=None):
+        return self._binary(lib().fhe_rns_polymul_batch, a, b, out)
+
+    def pointwise_multiply(self, a, b, out=None):
+        return self._binary(lib().fhe_rns_pointwise_batch, a, b, out)
+
+    def add(self, a, b, out=None):
+        return self._binary(lib().fhe_rns_add_batch, a, b, out)
+
+    def subtract(self, a, b, out=None):
+        return self._binary(lib().fhe_rns_sub_batch, a, b, out)
 
 
 class ExternalProduct:

@@ -139,3 +139,12 @@ def test_static_helpers_match_reference(golden_dir):
         assert P.mod_pow(b, e, m) == r
     for n, q, psi in kat["psi_table"]:
         assert P.find_primitive_root(n, q) == psi
+
+
+def test_rns_ring_validation():
+    """PolynomialRing(degree, moduli) with no modulus (polynomial_ring.cpp:
+    228-230) fails before any device work."""
+    import fhe_gpu
+
+    with pytest.raises(fhe_gpu.FHEError, match="At least one modulus required"):
+        fhe_gpu.RNSPolynomialRing(1024, [])

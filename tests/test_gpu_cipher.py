@@ -261,3 +261,35 @@ def test_cipher_golden_gpu(fg, golden_dir):
             be.blind_rotate(got, U(c["lwe_a"], 1, c["dim"]), U([c["lwe_b"]], 1),
                             be.prepare_ggsw(U(c["bsk"], c["dim"], 2 * c["level"], 2, n)))
         assert [int(v) for v in got.ravel()] == c["out"], (c["op"], n, q)
+
+
+# ------------------------------------------------------------ RNS ring
+@pytest.mark.parametrize("n,moduli", [(4096, [P27, P62, 40961, 12289]), (16384, [P27, P62]), (32768, [P27])])
+def test_rns_ring_vs_oracle(fg, n, moduli):
+    b = 2
+    r = fg.RNSPolynomialRing(n, moduli)
+    x = np.stack([rnd(100 + i, q, b, n) for i, q in enumerate(moduli)])
+    y = np.stack([rnd(200 + i, q, b, n) for i, q in enumerate(moduli)])
+    fx, ix, pm = r.forward_ntt(x), r.inverse_ntt(x), r.multiply(x, y)
+    pw, ad, sb = r.pointwise_multiply(x, y), r.add(x, y), r.subtract(x, y)
+    for i, q in enumerate(moduli):
+        t = oracle.NTT(n, q)
+        assert (fx[i] == t.forward(x[i])).all(), q
+        assert (ix[i] == t.inverse(x[i])).all(), q
+        assert (pm[i] == t.polymul(x[i], y[i])).all(), q
+        assert (pw[i] == oracle.pointwise(q, x[i].ravel(), y[i].ravel()).reshape(b, n)).all(), q
+        assert (ad[i] == oracle.poly_add(q, x[i].ravel(), y[i].ravel()).reshape(b, n)).all(), q
+        assert (sb[i] == oracle.poly_sub(q, x[i].ravel(), y[i].ravel()).reshape(b, n)).all(), q
+
+
+def test_rns_ring_device_and_errors(fg):
+    import torch
+
+    n, moduli = 1024, [P27, P62]
+    r = fg.RNSPolynomialRing(n, moduli)
+    x = np.stack([rnd(300 + i, q, 3, n) for i, q in enumerate(moduli)])
+    dev = r.forward_ntt(torch.from_numpy(x.view(np.int64)).cuda())
+    torch.cuda.synchronize()
+    assert (dev.cpu().numpy().view(np.uint64) == r.forward_ntt(x)).all()
+    with pytest.raises(fg.FHEError, match="NTT-friendly"):
+        fg.RNSPolynomialRing(n, [P27, 97])
