@@ -264,7 +264,7 @@ def test_cipher_golden_gpu(fg, golden_dir):
 
 
 # ------------------------------------------------------------ RNS ring
-@pytest.mark.parametrize("n,moduli", [(4096, [P27, P62, 40961, 12289]), (16384, [P27, P62]), (32768, [P27])])
+@pytest.mark.parametrize("n,moduli", [(4096, [P27, P62, 40961, 114689]), (16384, [P27, P62]), (32768, [P27])])
 def test_rns_ring_vs_oracle(fg, n, moduli):
     b = 2
     r = fg.RNSPolynomialRing(n, moduli)
