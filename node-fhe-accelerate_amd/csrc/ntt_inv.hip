@@ -83,7 +83,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     // P == 1: b's coefficients are loaded during fwd(a)'s last pass, so
     // their HBM latency overlaps it (one workgroup per CU has no other
     // workgroup to hide it behind).
-    constexpr bool PRE = G::P == 1 && FHE_POLY_PREFETCH && STASH != 0;
+    constexpr bool PRE = G::P == 1 && FHE_POLY_PREFETCH && STASH == 1;  // no registers to spare at STASH 2
     uint64_t rb[PRE ? G::E : 1];
     auto hook = [&] {
         if constexpr (PRE) load_raw<LOGN>(*reinterpret_cast<uint64_t(*)[G::E]>(rb), tau, b + poly * G::N);
@@ -95,14 +95,14 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);  // own positions: no sync needed
         if constexpr (STASH == 0) va[e] = x;
         else if constexpr (STASH == 1) st[gi] = x;
-        else if (valid) crow[gi] = (uint64_t)x;
+        else if (valid) reinterpret_cast<W *>(crow)[gi] = x;  // W-typed: first half of c's row
     }
     if constexpr (G::NP > 1) __syncthreads();  // LDS exchange buffer is reused by the second transform
     // opaque copy of the lane index (u64 path): stops the compiler from
     // keeping the first transform's address arithmetic live for reuse.  At
     // u32 the reuse is cheaper than recomputing (measured, r05 A/B).
     uint32_t tb = tau;
-    if constexpr (sizeof(W) == 8) asm volatile("" : "+v"(tb));
+    if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(tb));
     if constexpr (PRE)
         fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A, 0, 0, NoHook{},
                                                reinterpret_cast<uint64_t(*)[G::E]>(rb));
@@ -114,12 +114,12 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
         W x;
         if constexpr (STASH == 0) x = va[e];
         else if constexpr (STASH == 1) x = st[gi];
-        else x = valid ? (W)crow[gi] : W(0);
+        else x = valid ? reinterpret_cast<const W *>(crow)[gi] : W(0);
         v[e] = A.ar.mont(x, v[e]);  // a*b*R^-1 in [0, 2q): canonical x raw v[e] (< R)
     }
     if constexpr (G::NP > 1) __syncthreads();
     uint32_t ti = tau;
-    if constexpr (sizeof(W) == 8) asm volatile("" : "+v"(ti));
+    if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(ti));
     inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, ti, crow, valid, A, A.ninv_r, A.untwist_r);
 }
 
