@@ -148,3 +148,21 @@ def test_rns_ring_validation():
 
     with pytest.raises(fhe_gpu.FHEError, match="At least one modulus required"):
         fhe_gpu.RNSPolynomialRing(1024, [])
+
+
+def test_parameter_presets():
+    """parameter_set.cpp presets as data, and which moduli the GPU can run
+    (Q_40_1, Q_40_2, Q_50_2 are composite; Q_50_1 stops at N = 8192)."""
+    from fhe_gpu import params as P
+
+    assert P.create_parameter_set("tfhe-128-fast").lwe_dimension == 742
+    with pytest.raises(ValueError, match="Unknown parameter preset: nope"):
+        P.create_parameter_set("nope")
+    assert P.Q_40_1 == 257 * 4278255361
+    assert not P._is_prime(P.Q_40_1) and not P._is_prime(P.Q_40_2) and not P._is_prime(P.Q_50_2)
+    assert P._is_prime(P.Q_60_1) and P._is_prime(P.Q_50_1) and P._is_prime(132120577)
+    fast = P.gpu_moduli(P.create_parameter_set("tfhe-128-fast"))
+    assert not fast[0]["usable"]
+    ckks = P.gpu_moduli(P.create_parameter_set("ckks-128-ml"))
+    assert [m["usable"] for m in ckks] == [True, False, False, False, False]  # only Q_60_1 admits N = 16384
+    assert all(m["usable"] for m in P.gpu_moduli(P.create_parameter_set("bfv-128-simd")))

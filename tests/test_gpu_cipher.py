@@ -293,3 +293,33 @@ def test_rns_ring_device_and_errors(fg):
     assert (dev.cpu().numpy().view(np.uint64) == r.forward_ntt(x)).all()
     with pytest.raises(fg.FHEError, match="NTT-friendly"):
         fg.RNSPolynomialRing(n, [P27, 97])
+
+
+# ------------------------------------------------------------ reference parameter presets
+def test_presets_bfv_rns_and_tfhe_balanced(fg):
+    """bfv-128-simd's modulus chain as an RNS ring, and tfhe-128-balanced's
+    (N, q, B, L) through CMux + blind rotation (parameter_set.cpp:139-224)."""
+    from fhe_gpu import params as P
+
+    bfv = P.create_parameter_set("bfv-128-simd")
+    n = bfv.poly_degree
+    r = fg.RNSPolynomialRing(n, bfv.moduli)
+    x = np.stack([rnd(400 + i, q, 1, n) for i, q in enumerate(bfv.moduli)])
+    y = np.stack([rnd(500 + i, q, 1, n) for i, q in enumerate(bfv.moduli)])
+    pm = r.multiply(x, y)
+    for i, q in enumerate(bfv.moduli):
+        assert (pm[i] == oracle.NTT(n, q).polymul(x[i], y[i])).all(), q
+
+    tb = P.create_parameter_set("tfhe-128-balanced")
+    n, q, bl, lv, dim = tb.poly_degree, tb.moduli[0], tb.decomp_base_log, tb.decomp_level, 6
+    ring = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(ring, bl, lv, 1)
+    bsk = rnd(601, q, dim, 2 * lv, 2, n)
+    lwe_a, lwe_b = rnd(602, q, 2, dim), rnd(603, q, 2)
+    acc0 = np.zeros((2, 2, n), np.uint64)
+    acc0[:, 1] = rnd(604, q, 2, n)
+    acc = acc0.copy()
+    be.blind_rotate(acc, lwe_a, lwe_b, be.prepare_ggsw(bsk))
+    for i in range(2):
+        assert (acc[i] == t.blind_rotate(1, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])).all(), i
