@@ -40,10 +40,21 @@ namespace FHE_NS {
 // region, 2 = the ciphertext's own output rows in HBM (read-modify-write of
 // the thread's own positions; no synchronisation needed).  Holding them in
 // VGPRs spilled 300-800 B/lane.
+// LDS accumulators are used only while they leave at least kExtMinWaves
+// waves per CU resident: at N = 1024 with u64 words they would cut the CU to
+// one 4-wave workgroup (99 KB of LDS), and the HBM/L2 round trip of the
+// output-row stash is cheaper than that loss of latency hiding.
+#ifndef FHE_EXT_MINWAVES
+#define FHE_EXT_MINWAVES 8
+#endif
+constexpr int kExtMinWaves = FHE_EXT_MINWAVES;
 template <int LOGN, typename W, int K1>
 constexpr int ext_stash() {
     using G = Geo<LOGN>;
-    return G::P * (G::LW + K1 * G::N) * (int)sizeof(W) <= 160 * 1024 ? 1 : 2;
+    constexpr int bytes = G::P * (G::LW + K1 * G::N) * (int)sizeof(W);
+    if (bytes > 160 * 1024) return 2;
+    const int wg = (160 * 1024) / bytes < 2048 / G::THREADS ? (160 * 1024) / bytes : 2048 / G::THREADS;
+    return wg * G::THREADS / 64 >= kExtMinWaves ? 1 : 2;
 }
 template <int LOGN, typename W, int K1>
 constexpr int ext_extra_words() {
