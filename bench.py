@@ -183,6 +183,46 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
                                   "achieved_GBs": 40 * n * B / (kms * 1e-3) / 1e9}
             del out, ek
         del x, y, ct3
+    if only in ("", "c5"):
+        # C5 (BASELINE.json configs[4]): TFHE external product at N=16384,
+        # q = 62-bit prime, k=1, (B, L) in {(23, 1), (15, 2)}, a batch of GLWE
+        # ciphertexts against one GGSW; plus the 2-limb Montgomery batch.
+        n, q, B = 16384, P62, 4096
+        ring = fhe_gpu.PolynomialRing(n, q, device=dev)
+        glwe = torch.randint(0, q, (B, 2, n), device="cuda", dtype=torch.int64, generator=g)
+        out = torch.empty_like(glwe)
+        c5 = {"n": n, "q": q, "k": 1, "batch": B}
+        for bl, lv in ((23, 1), (15, 2)):
+            ggsw = torch.randint(0, q, (2 * lv, 2, n), device="cuda", dtype=torch.int64, generator=g)
+            ep = fhe_gpu.ExternalProduct(ring, ggsw, bl, lv)
+            wall, kms = timed(dist, lambda: ep(glwe, out=out), steps, warmup)
+            c5[f"extprod_B{bl}_L{lv}"] = {"per_s": B * steps / wall, "kernel_ms": kms,
+                                          "transforms_per_unit": 2 * lv + 2}
+        del glwe, out
+        cnt = 16384 * 1024
+        ml = fhe_gpu.MultiLimbModularArithmetic([0xFFFFFFFF00000001, 0x3FFFFFFFFFFFFFFF])
+        ma = torch.randint(0, 1 << 62, (cnt, 2), device="cuda", dtype=torch.int64, generator=g)
+        mb = torch.randint(0, 1 << 62, (cnt, 2), device="cuda", dtype=torch.int64, generator=g)
+        mo = torch.empty_like(ma)
+        wall, kms = timed(dist, lambda: ml.montgomery_mul_batch(ma, mb, out=mo), steps, warmup)
+        c5["ml_montmul_2limb"] = {"count": cnt, "per_s": cnt * steps / wall, "kernel_ms": kms,
+                                  "achieved_GBs": 48 * cnt / (kms * 1e-3) / 1e9}
+        res["c5"] = c5
+        del ma, mb, mo
+    if only in ("", "c2"):
+        # C2 (configs[1]): N=4096 fwd + inv NTT and polymul, batch 1024
+        n, q, B = 4096, P27, 1024
+        ring = fhe_gpu.PolynomialRing(n, q, device=dev)
+        a = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
+        b = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
+        o = torch.empty_like(a)
+        c2 = {"n": n, "q": q, "batch": B}
+        for name, fn in (("fwd", lambda: ring.forward_ntt(a, out=o)), ("inv", lambda: ring.inverse_ntt(a, out=o)),
+                         ("polymul", lambda: ring.multiply(a, b, out=o))):
+            wall, kms = timed(dist, fn, steps * 4, warmup)
+            c2[name] = {"per_s": B * steps * 4 / wall, "kernel_ms": kms}
+        res["c2"] = c2
+        del a, b, o
     if only in ("", "blind_rotate"):
         # tfhe-128-fast shape (parameter_set.cpp): N=1024, k=1, B=23, L=1, n=742;
         # q = the 62-bit prime (Q_40_1 = 2^40+1 is not prime)
@@ -254,7 +294,7 @@ def main():
 
     n, B, K, W = args.n, args.batch, args.steps, args.warmup
     extra = {}
-    if args.only in ("ct_mul", "relin", "blind_rotate"):  # profiling runs of the side metrics
+    if args.only in ("ct_mul", "relin", "blind_rotate", "c5", "c2"):  # profiling runs of the side metrics
         c = cipher_workload(fhe_gpu, K, W, dist, args.only)
         if rank == 0:
             print(json.dumps({"cipher": c}), flush=True)
