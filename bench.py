@@ -352,7 +352,12 @@ def main():
         pw, pk = r["polymul"]
         line["polymuls_per_s"] = world * B * K / pw
         line["polymul_roofline"] = {"achieved": 24 * n * B / (pk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                                    "unit": "GB/s", "kernel_ms": pk}
+                                    "unit": "GB/s", "kernel_ms": pk,
+                                    "bound": "valu (3 transforms per 24N bytes; DESIGN.md section 6)"}
+        trp = pmc_traffic("polymul", n, B, args.q)
+        if trp:
+            line["polymul_roofline"]["traffic"] = trp[0]
+            line["polymul_roofline"]["traffic_source"] = trp[1]
     line.update(extra)
     if not args.no_cpu and world == 1 and not args.only:
         line["cpu_baseline"] = cpu_baseline(n, args.q, args.cpu_seconds)
