@@ -590,6 +590,50 @@ class EncryptionEngine:
     def __init__(self, ring: "PolynomialRing"):
         self.ring = ring
 
+    def _pair(self, ct1, ct2):
+        ct1, ct2 = _as_u64(ct1), _as_u64(ct2)
+        _lead(ct1, (2, self.ring.degree))
+        if tuple(ct2.shape) != tuple(ct1.shape):
+            raise FHEError(-9, "ciphertext shapes differ")
+        return ct1, ct2
+
+    def add(self, ct1, ct2, out=None):
+        """add (:594-617): componentwise mod_add of (c0, c1)."""
+        ct1, ct2 = self._pair(ct1, ct2)
+        return self.ring.add(ct1, ct2, out)
+
+    def subtract(self, ct1, ct2, out=None):
+        """subtract (:692-714)."""
+        ct1, ct2 = self._pair(ct1, ct2)
+        return self.ring.subtract(ct1, ct2, out)
+
+    def negate(self, ct, out=None):
+        """negate (:716-727)."""
+        ct = _as_u64(ct)
+        _lead(ct, (2, self.ring.degree))
+        return self.ring.negate(ct, out)
+
+    def multiply_scalar(self, ct, scalar: int, out=None):
+        """multiply_scalar (:890-902)."""
+        ct = _as_u64(ct)
+        _lead(ct, (2, self.ring.degree))
+        return self.ring.multiply_scalar(ct, scalar, out)
+
+    def multiply_plain(self, ct, pt, out=None):
+        """multiply_plain (:809-850) for an already-encoded plaintext
+        polynomial pt [..., n] (one per ciphertext, or one for all): each
+        component times pt through the fused polymul (coefficient form)."""
+        r = self.ring
+        ct = _as_u64(ct)
+        nb = _lead(ct, (2, r.degree))
+        pt = _as_u64(pt)
+        if _is_tensor(ct):
+            ptb = pt.reshape(-1, 1, r.degree).expand(nb, 2, r.degree).reshape(ct.shape).contiguous()
+        else:
+            ptb = np.ascontiguousarray(np.broadcast_to(np.asarray(pt).reshape(-1, 1, r.degree),
+                                                       (nb, 2, r.degree)).reshape(ct.shape))
+        return r.multiply(ct, ptb, out)
+
     def multiply(self, ct1, ct2, is_ntt: bool = False, out=None):
         """multiply (:737-798): tensor product -> [..., 3, n]."""
         r = self.ring
@@ -606,9 +650,15 @@ class EncryptionEngine:
         return out
 
     def relinearize(self, ct3, ek: EvaluationKey, out=None):
-        """relinearize (:904-980): [..., 3, n] -> [..., 2, n]."""
+        """relinearize (:904-980): [..., 3, n] -> [..., 2, n]; a degree-1
+        input [..., 2, n] is returned as a copy (:906-909)."""
         r = self.ring
         ct3 = _as_u64(ct3)
+        if len(ct3.shape) >= 2 and tuple(ct3.shape[-2:]) == (2, r.degree):
+            if out is None:
+                return ct3.clone() if _is_tensor(ct3) else ct3.copy()
+            out[...] = ct3
+            return out
         nb = _lead(ct3, (3, r.degree))
         if out is None:
             out = _empty(ct3, tuple(ct3.shape[:-2]) + (2, r.degree))

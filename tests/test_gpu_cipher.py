@@ -323,3 +323,27 @@ def test_presets_bfv_rns_and_tfhe_balanced(fg):
     be.blind_rotate(acc, lwe_a, lwe_b, be.prepare_ggsw(bsk))
     for i in range(2):
         assert (acc[i] == t.blind_rotate(1, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])).all(), i
+
+
+def test_ciphertext_linear_ops_and_plain(fg):
+    """EncryptionEngine::add / subtract / negate / multiply_scalar /
+    multiply_plain (encryption.cpp:594-902) and relinearize of a degree-1
+    ciphertext (a copy, :906-909)."""
+    n, q, b = 1024, P27, 3
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    eng = fg.EncryptionEngine(r)
+    x, y = rnd(701, q, b, 2, n), rnd(702, q, b, 2, n)
+    x[0, 0, :3] = [2**64 - 1, q, 0]
+    pt = rnd(703, q, n)
+    add, sub, neg = eng.add(x, y), eng.subtract(x, y), eng.negate(x)
+    sc, pm = eng.multiply_scalar(x, 2**63 + 12345), eng.multiply_plain(x, pt)
+    for i in range(b):
+        for j in range(2):
+            assert (add[i, j] == oracle.poly_add(q, x[i, j], y[i, j])).all()
+            assert (sub[i, j] == oracle.poly_sub(q, x[i, j], y[i, j])).all()
+            assert (neg[i, j] == oracle.poly_neg(q, x[i, j])).all()
+            assert (sc[i, j] == oracle.poly_mul_scalar(q, x[i, j], 2**63 + 12345)).all()
+            assert (pm[i, j] == t.polymul(x[i, j], pt)).all()
+    ek = fg.EvaluationKey(r, rnd(704, q, 3, 2, n), 4)
+    assert (eng.relinearize(x, ek) == x).all()
