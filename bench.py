@@ -238,7 +238,13 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
         res["blind_rotate"] = {"n": n, "q": q, "k": 1, "base_log": bl, "level": lv, "lwe_dim": dim, "batch": B,
                                "per_s": B * st / wall, "ms_per_batch": kms,
                                "cmux_per_s": B * dim * st / wall}
-        del bsk, lwe_a, lwe_b, acc
+        # latency of a small batch (64 ciphertexts): launch-bound, replayed as a hipGraph
+        Bs = 64
+        acc_s, la_s, lb_s = acc[:Bs].contiguous(), lwe_a[:Bs].contiguous(), lwe_b[:Bs].contiguous()
+        wall, kms = timed(dist, lambda: be.blind_rotate(acc_s, la_s, lb_s, bsk), st * 4, 1)
+        res["blind_rotate"]["batch64_ms"] = kms
+        res["blind_rotate"]["batch64_per_s"] = Bs * st * 4 / wall
+        del bsk, lwe_a, lwe_b, acc, acc_s, la_s, lb_s
     torch.cuda.empty_cache()
     return res
 

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -97,6 +98,21 @@ struct fhe_ctx {
     std::mutex scratch_mu;
     void *scratch[3] = {nullptr, nullptr, nullptr};
     size_t scratch_bytes = 0;
+    // blind rotation: ping-pong accumulator buffer and the captured launch
+    // sequence (1 rotation + lwe_dim CMux steps + copy) as a hipGraph, reused
+    // while the call's buffers and shape are unchanged
+    struct BrGraph {
+        const void *acc = nullptr, *lwe_a = nullptr, *lwe_b = nullptr, *bsk = nullptr;
+        size_t batch = 0;
+        uint32_t k = 0, base_log = 0, level = 0, dim = 0;
+        uint64_t lwe_q = 0;
+        hipStream_t stream = nullptr;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+    } br;
+    std::mutex br_mu;
+    void *br_tmp = nullptr;
+    size_t br_tmp_bytes = 0;
 };
 
 namespace {
@@ -190,6 +206,11 @@ void free_tables(fhe_ctx *c) {
         if (s) { (void)hipFree(s); s = nullptr; }
     for (auto &s : c->plan.big_scratch)
         if (s) { (void)hipFree(s); s = nullptr; }
+    if (c->br.exec) (void)hipGraphExecDestroy(c->br.exec);
+    if (c->br.graph) (void)hipGraphDestroy(c->br.graph);
+    c->br = fhe_ctx::BrGraph{};
+    if (c->br_tmp) { (void)hipFree(c->br_tmp); c->br_tmp = nullptr; }
+    c->br_tmp_bytes = 0;
 }
 
 FHE_NS::ModConsts mod_consts(u64 q) {
@@ -825,21 +846,69 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
     FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
     FHE_TRY(hs.map(where, acc, bytes, 3));
-    u64 *tmp = nullptr;
-    HIP_TRY(hipMalloc((void **)&tmp, bytes), "hipMalloc(blind rotate)");
-    // acc <- X^-round(b 2N / q) acc, into tmp; then lwe_dim CMux steps
-    // ping-ponging tmp <-> acc; the result is copied back into acc if the
-    // step count is even (it ended in tmp).
-    hipError_t e = FHE_NS::launch_rotate(mod_consts(c->q), acc, tmp, c->n, k + 1, batch, nullptr, lwe_b, lwe_q, c->stream);
-    u64 *cur = tmp, *nxt = acc;
-    for (uint32_t i = 0; e == hipSuccess && i < lwe_dim; ++i) {
-        e = FHE_NS::launch_cmux_rotate(c->plan, (int)k + 1, (int)level, (int)base_log, cur, bsk_ntt + ggsw_words * i, nxt,
-                                       batch, lwe_a, lwe_dim, i, lwe_q);
-        std::swap(cur, nxt);
+    std::lock_guard<std::mutex> lk(c->br_mu);
+    if (c->br_tmp_bytes < bytes) {
+        if (c->br.exec) { (void)hipGraphExecDestroy(c->br.exec); c->br.exec = nullptr; }
+        if (c->br.graph) { (void)hipGraphDestroy(c->br.graph); c->br.graph = nullptr; }
+        if (c->br_tmp) (void)hipFree(c->br_tmp);
+        c->br_tmp = nullptr;
+        c->br_tmp_bytes = 0;
+        HIP_TRY(hipMalloc(&c->br_tmp, bytes), "hipMalloc(blind rotate)");
+        c->br_tmp_bytes = bytes;
     }
-    if (e == hipSuccess && cur != acc) e = hipMemcpyAsync(acc, cur, bytes, hipMemcpyDeviceToDevice, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(tmp);
+    u64 *tmp = (u64 *)c->br_tmp;
+    // acc <- X^-round(b 2N / q) acc, into tmp; then lwe_dim CMux steps
+    // ping-ponging tmp <-> acc; the result is copied back into acc if it
+    // ended in tmp.
+    auto enqueue = [&]() -> hipError_t {
+        hipError_t e = FHE_NS::launch_rotate(mod_consts(c->q), acc, tmp, c->n, k + 1, batch, nullptr, lwe_b, lwe_q,
+                                             c->stream);
+        u64 *cur = tmp, *nxt = acc;
+        for (uint32_t i = 0; e == hipSuccess && i < lwe_dim; ++i) {
+            e = FHE_NS::launch_cmux_rotate(c->plan, (int)k + 1, (int)level, (int)base_log, cur,
+                                           bsk_ntt + ggsw_words * i, nxt, batch, lwe_a, lwe_dim, i, lwe_q);
+            std::swap(cur, nxt);
+        }
+        if (e == hipSuccess && cur != acc) e = hipMemcpyAsync(acc, cur, bytes, hipMemcpyDeviceToDevice, c->stream);
+        return e;
+    };
+    // Device-resident calls: the lwe_dim + 2 launches are captured once into
+    // a hipGraph and replayed while (buffers, shape, stream) are unchanged.
+    // The legacy null stream cannot be captured; FHE_NO_GRAPH=1 disables
+    // graphs.
+    static const bool no_graph = std::getenv("FHE_NO_GRAPH") && std::getenv("FHE_NO_GRAPH")[0] == '1';
+    fhe_ctx::BrGraph &G = c->br;
+    const bool same = G.exec && G.acc == acc && G.lwe_a == lwe_a && G.lwe_b == lwe_b && G.bsk == bsk_ntt &&
+                      G.batch == batch && G.k == k && G.base_log == base_log && G.level == level &&
+                      G.dim == lwe_dim && G.lwe_q == lwe_q && G.stream == c->stream;
+    hipError_t e = hipSuccess;
+    if (!no_graph && where == FHE_DEVICE && c->stream != nullptr && lwe_dim > 0) {
+        if (!same) {
+            if (G.exec) (void)hipGraphExecDestroy(G.exec);
+            if (G.graph) (void)hipGraphDestroy(G.graph);
+            G = fhe_ctx::BrGraph{};
+            hipGraph_t graph = nullptr;
+            hipGraphExec_t exec = nullptr;
+            e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed);
+            if (e == hipSuccess) {
+                hipError_t e1 = enqueue();
+                hipError_t e2 = hipStreamEndCapture(c->stream, &graph);
+                e = e1 != hipSuccess ? e1 : e2;
+            }
+            if (e == hipSuccess) e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+            if (e == hipSuccess) {
+                G.acc = acc; G.lwe_a = lwe_a; G.lwe_b = lwe_b; G.bsk = bsk_ntt; G.batch = batch; G.k = k;
+                G.base_log = base_log; G.level = level; G.dim = lwe_dim; G.lwe_q = lwe_q; G.stream = c->stream;
+                G.graph = graph; G.exec = exec;
+            } else {
+                if (graph) (void)hipGraphDestroy(graph);
+                (void)hipGetLastError();
+            }
+        }
+        e = G.exec ? hipGraphLaunch(G.exec, c->stream) : enqueue();
+    } else {
+        e = enqueue();
+    }
     if (e != hipSuccess) return hip_fail(e, "blind rotate");
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
