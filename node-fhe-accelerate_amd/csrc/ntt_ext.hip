@@ -48,22 +48,29 @@ namespace FHE_NS {
 #define FHE_EXT_MINWAVES 8
 #endif
 constexpr int kExtMinWaves = FHE_EXT_MINWAVES;
-template <int LOGN, typename W, int K1>
+template <int LOGN, typename W, int K1, int MODE = 0>
 constexpr int ext_stash() {
     using G = Geo<LOGN>;
     constexpr int bytes = G::P * (G::LW + K1 * G::N) * (int)sizeof(W);
-    if (bytes > 160 * 1024) return 2;
-    const int wg = (160 * 1024) / bytes < 2048 / G::THREADS ? (160 * 1024) / bytes : 2048 / G::THREADS;
-    return wg * G::THREADS / 64 >= kExtMinWaves ? 1 : 2;
+    if (bytes <= 160 * 1024) {
+        const int wg = (160 * 1024) / bytes < 2048 / G::THREADS ? (160 * 1024) / bytes : 2048 / G::THREADS;
+        if (wg * G::THREADS / 64 >= kExtMinWaves) return 1;
+    }
+    // relinearisation (MODE 1): accumulator 0 in LDS, accumulator 1 and the
+    // c2 words in VGPRs (one workgroup per CU); c2 is then read once instead
+    // of once per digit level
+    if (MODE == 1 && K1 == 2 && G::P == 1 && (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024) return 3;
+    return 2;
 }
-template <int LOGN, typename W, int K1>
+template <int LOGN, typename W, int K1, int MODE = 0>
 constexpr int ext_extra_words() {
-    return ext_stash<LOGN, W, K1>() == 1 ? Geo<LOGN>::P * K1 * Geo<LOGN>::N : 0;
+    constexpr int st = ext_stash<LOGN, W, K1, MODE>();
+    return st == 1 ? Geo<LOGN>::P * K1 * Geo<LOGN>::N : (st == 3 ? Geo<LOGN>::N : 0);
 }
 
-template <int LOGN, typename W, int K1>
+template <int LOGN, typename W, int K1, int MODE = 0>
 constexpr int ext_occ() {
-    constexpr int extra = ext_extra_words<LOGN, W, K1>();
+    constexpr int extra = ext_extra_words<LOGN, W, K1, MODE>();
     return Geo<LOGN>::template occ_waves<W, extra>();
 }
 
@@ -80,12 +87,12 @@ struct DmArgs {
 };
 
 template <int LOGN, typename W, bool NEGA, int K1, bool LAZY, int MODE>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ext_occ<LOGN, W, K1>()))
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ext_occ<LOGN, W, K1, MODE>()))
 k_dmac(DmArgs D, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    constexpr int STASH = ext_stash<LOGN, W, K1>();
+    constexpr int STASH = ext_stash<LOGN, W, K1, MODE>();
     constexpr int NIN = MODE == 1 ? 3 : K1;  // source polynomials per ciphertext
-    __shared__ W lds_all[G::P * G::LW + ext_extra_words<LOGN, W, K1>()];
+    __shared__ W lds_all[G::P * G::LW + ext_extra_words<LOGN, W, K1, MODE>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < D.batch;
@@ -94,10 +101,18 @@ k_dmac(DmArgs D, NttArgs<W> A) {
     uint64_t *orow = D.out + poly * K1 * G::N;
     const uint64_t *srow = D.src + (valid ? poly : 0) * NIN * G::N;
     // accumulator j of this ciphertext: LDS, or row j of the output
+    // (STASH 3: j = 0 only; accumulator 1 is racc)
     auto acc = [&](int j) -> W * {
         if constexpr (STASH == 1) return lds_all + G::P * G::LW + (pl * K1 + j) * G::N;
+        else if constexpr (STASH == 3) return lds_all + G::LW;
         else return reinterpret_cast<W *>(orow + (size_t)j * G::N);
     };
+    W racc[STASH == 3 ? G::E : 1];
+    uint64_t craw[STASH == 3 ? G::E : 1];  // c2 words at this lane's pass-0 positions
+    if constexpr (STASH == 3) {
+#pragma unroll
+        for (int t = 0; t < G::E; ++t) craw[t] = valid ? srow[2 * G::N + tau + cbrv(t, G::LOGE) * G::T] : 0;
+    }
 
     const int level = D.level;
     const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
@@ -132,7 +147,8 @@ k_dmac(DmArgs D, NttArgs<W> A) {
             const uint32_t p = tr + cbrv(t, G::LOGE) * G::T;
             if (!valid || skip) return 0;
             uint64_t c;
-            if constexpr (MODE == 2) c = subq(red_q(rotated_at(src, p, rot, G::N, q, mu), q, mu), red_q(src[p], q, mu), q);
+            if constexpr (STASH == 3) c = craw[STASH == 3 ? t : 0];
+            else if constexpr (MODE == 2) c = subq(red_q(rotated_at(src, p, rot, G::N, q, mu), q, mu), red_q(src[p], q, mu), q);
             else if constexpr (MODE == 3) c = subq(red_q(src2[p], q, mu), red_q(src[p], q, mu), q);
             else c = src[p];
             uint64_t d = (c >> shift) & mask;
@@ -162,7 +178,8 @@ k_dmac(DmArgs D, NttArgs<W> A) {
                     const uint32_t gi = gidx<LOGN, G::NP - 1>(tr, c0 + e);
                     const int kj = MODE == 1 ? 1 - j : j;  // relin: c0' uses b_l, c1' uses a_l
                     kv[e][j] = g[(size_t)kj * G::N + gi];
-                    pv[e][j] = r == 0 ? W(0) : acc(j)[gi];
+                    if (STASH == 3 && j > 0) pv[e][j] = r == 0 ? W(0) : racc[STASH == 3 ? c0 + e : 0];
+                    else pv[e][j] = r == 0 ? W(0) : acc(j)[gi];
                 }
 #pragma unroll
             for (int e = 0; e < 2; ++e)
@@ -170,18 +187,23 @@ k_dmac(DmArgs D, NttArgs<W> A) {
                 for (int j = 0; j < K1; ++j) {
                     // raw output (< R) times a canonical key: valid Montgomery pair
                     const W m = A.ar.mont(v[c0 + e], (W)kv[e][j]);
-                    acc(j)[gidx<LOGN, G::NP - 1>(tr, c0 + e)] = A.ar.red2q(pv[e][j] + m);
+                    if (STASH == 3 && j > 0) racc[STASH == 3 ? c0 + e : 0] = A.ar.red2q(pv[e][j] + m);
+                    else acc(j)[gidx<LOGN, G::NP - 1>(tr, c0 + e)] = A.ar.red2q(pv[e][j] + m);
                 }
         }
     }
-#pragma nounroll
-    for (int j = 0; j < K1; ++j) {
+    auto out_row = [&](int j) {
         if (G::NP > 1) __syncthreads();
         uint32_t tr = tau;
         asm volatile("" : "+v"(tr));
         W v[G::E];
+        if (STASH == 3 && j > 0) {
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) v[e] = valid ? acc(j)[gidx<LOGN, G::NP - 1>(tr, e)] : W(0);
+            for (int e = 0; e < G::E; ++e) v[e] = valid ? racc[STASH == 3 ? e : 0] : W(0);
+        } else {
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) v[e] = valid ? acc(j)[gidx<LOGN, G::NP - 1>(tr, e)] : W(0);
+        }
         if constexpr (STASH == 2) {
             if (G::NP > 1) __syncthreads();  // every stash read of row j precedes its final stores
         }
@@ -198,6 +220,13 @@ k_dmac(DmArgs D, NttArgs<W> A) {
             }
         };
         inv_poly_from_regs<LOGN, NEGA>(lds, v, tr, orow + (size_t)j * G::N, valid, A, A.ninv, A.untwist, 0, 0, fin);
+    };
+    if constexpr (STASH == 3) {  // unrolled: racc is indexed by the row
+#pragma unroll
+        for (int j = 0; j < K1; ++j) out_row(j);
+    } else {
+#pragma nounroll
+        for (int j = 0; j < K1; ++j) out_row(j);
     }
 }
 
