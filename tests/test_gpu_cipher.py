@@ -347,3 +347,33 @@ def test_ciphertext_linear_ops_and_plain(fg):
             assert (pm[i, j] == t.polymul(x[i, j], pt)).all()
     ek = fg.EvaluationKey(r, rnd(704, q, 3, 2, n), 4)
     assert (eng.relinearize(x, ek) == x).all()
+
+
+@pytest.mark.parametrize("n,q,bl,lv", [(16384, P27, 4, 7), (4096, P62, 16, 4)])
+def test_decryption_identity_negacyclic(fg, n, q, bl, lv):
+    """Size-independent property at full degree: in the negacyclic ring,
+    noise-free ciphertexts ct_i = (m_i - a_i s, a_i) satisfy
+      c0 + c1 s + c2 s^2 = m1 m2              after multiply, and
+      c0' + c1' s       = m1 m2              after relinearize,
+    with rlk_l = (a_l, s^2 B^l - a_l s) (key_manager.cpp:296-324 without noise)."""
+    b = 8
+    r = fg.PolynomialRing(n, q, mode="negacyclic")
+    eng = fg.EncryptionEngine(r)
+    s = rnd(801, q, n)
+    S = np.broadcast_to(s, (b, n)).copy()
+    m1, m2, a1, a2 = rnd(802, q, b, n), rnd(803, q, b, n), rnd(804, q, b, n), rnd(805, q, b, n)
+    ct1 = np.stack([r.subtract(m1, r.multiply(a1, S)), a1], axis=1)
+    ct2 = np.stack([r.subtract(m2, r.multiply(a2, S)), a2], axis=1)
+    ct3 = eng.multiply(ct1, ct2)
+    s2 = r.multiply(S, S)
+    dec3 = r.add(r.add(ct3[:, 0], r.multiply(ct3[:, 1], S)), r.multiply(ct3[:, 2], s2))
+    want = r.multiply(m1, m2)
+    assert (dec3 == want).all()
+    al = rnd(806, q, lv, n)
+    s2_1 = s2[:lv]
+    scaled = np.stack([r.multiply_scalar(s2_1[l:l + 1], pow(1 << bl, l, q))[0] for l in range(lv)])
+    bl_keys = r.subtract(scaled, r.multiply(al, np.broadcast_to(s, (lv, n)).copy()))
+    rlk = np.stack([al, bl_keys], axis=1)
+    out = eng.relinearize(ct3, fg.EvaluationKey(r, rlk, bl))
+    dec2 = r.add(out[:, 0], r.multiply(out[:, 1], S))
+    assert (dec2 == want).all()
