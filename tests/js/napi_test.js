@@ -20,6 +20,7 @@ const goldenBig = (name) => {
 const U = (xs) => BigUint64Array.from(xs.map((x) => BigInt(x)));
 
 let passed = 0;
+const asyncTests = [];
 function test(name, fn) {
   fn();
   passed += 1;
@@ -114,6 +115,19 @@ if (mode === 'cpu') {
       assert.deepStrictEqual(Array.from(got), c.out.map(BigInt), `${c.op} n=${c.n}`);
     }
   });
+  test('createEngine: ciphertext multiply / relinearize vs golden (async FHEEngine surface)', () => {
+    const pending = [];
+    for (const c of goldenBig('cipher.json')) {
+      if (c.op === 'blind_rotate') continue;
+      const custom = { polyDegree: c.n, moduli: [BigInt(c.q)], decompBaseLog: c.base_log || 4 };
+      pending.push(fhe.createEngine(custom).then(async (eng) => {
+        const got = c.op === 'ct_multiply' ? await eng.multiply(U(c.ct1), U(c.ct2))
+          : await eng.relinearize(U(c.ct3), U(c.rlk), c.base_log);
+        assert.deepStrictEqual(Array.from(got), c.out.map(BigInt), `${c.op} n=${c.n}`);
+      }));
+    }
+    asyncTests.push(Promise.all(pending));
+  });
   test('negacyclic mode is the ring product', () => {
     for (const c of goldenBig('negacyclic.json')) {
       const e = new fhe.PolynomialEngine(c.n, BigInt(c.q), { mode: 'negacyclic' });
@@ -121,4 +135,7 @@ if (mode === 'cpu') {
     }
   });
 }
-console.log(`${passed} passed (${mode})`);
+Promise.all(asyncTests).then(() => console.log(`${passed} passed (${mode})`)).catch((e) => {
+  console.error(e);
+  process.exit(1);
+});
