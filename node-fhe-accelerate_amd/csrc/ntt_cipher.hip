@@ -87,7 +87,9 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     // HBM slots A/B are prefetched into registers during the last pass of
     // the transform that consumes them (their latency overlaps it; with one
     // workgroup per CU nothing else would hide it).
-    constexpr bool HB = NL == 1;  // NL == 0 (C in VGPRs) has no registers to spare
+    // (only the lab build FHE_CTMUL_AREG=0 keeps A/B in HBM at NL == 1;
+    // NL == 0 (C in VGPRs) has no registers to spare for the prefetch)
+    constexpr bool HB = NL == 1 && !AREG;
     W pre[2][HB ? G::E : 1];
     W v[G::E];
     // a fresh opaque copy of the lane index per phase: stops the compiler
