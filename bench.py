@@ -267,15 +267,16 @@ def pmc_traffic(kernel, n, batch, q):
     return best
 
 
-def cpu_baseline(n, q, seconds):
+def cpu_baseline(n, q, seconds, threads=None):
     """The oracle (C restatement of the reference NTTProcessor + pointwise,
     same % -based op sequence) on the host cores, bounded sample."""
     import oracle
 
-    try:
-        threads = min(16, len(os.sched_getaffinity(0)))
-    except Exception:
-        threads = 8
+    if threads is None:
+        try:
+            threads = min(16, len(os.sched_getaffinity(0)))
+        except Exception:
+            threads = 8
     t = oracle.NTT(n, q)
     chunk = threads * 2
     a = oracle.splitmix_fill(1, q, chunk * n).reshape(chunk, n)
@@ -367,6 +368,8 @@ def main():
     line.update(extra)
     if not args.no_cpu and world == 1 and not args.only:
         line["cpu_baseline"] = cpu_baseline(n, args.q, args.cpu_seconds)
+        # also one thread (the reference's sequential forward_ntt_batch)
+        line["cpu_baseline_1thread"] = cpu_baseline(n, args.q, min(4.0, args.cpu_seconds), threads=1)
         line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line), flush=True)
     if dist is not None:
