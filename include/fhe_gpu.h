@@ -194,7 +194,7 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  *   ciphertext c with its own LWE (lwe_a[c], lwe_b[c]) modulo lwe_q; bsk_ntt
  *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).
  * fhe_sample_extract_batch sample_extract (:594-624): lwe_a [batch][k*n].
- * fhe_key_switch_batch     key_switch (:630-677): ksk_a [in_dim*level][out_dim]
+ * fhe_key_switch_batch     key_switch (:626-674): ksk_a [in_dim*level][out_dim]
  *   (the `first` polynomials of ksk.keys, entry i*level + l), ksk_b
  *   [in_dim*level] (coefficient 0 of each `second` polynomial). */
 int fhe_glwe_rotate_batch(fhe_ctx *ctx, uint32_t k, const int32_t *rot, const uint64_t *glwe, uint64_t *out,

@@ -5,7 +5,7 @@
 //                  (bootstrap_engine.cpp:249-261, 122-145); also blind_rotate's
 //                  initial rotation by -round(b * 2N / q) (:555-557)
 //   sample_extract (:594-624)
-//   key_switch     (:630-677): out_a = -sum_{i,l} d_il * ksk_a[i,l]  (mod q),
+//   key_switch     (:626-674): out_a = -sum_{i,l} d_il * ksk_a[i,l]  (mod q),
 //                  out_b = b - sum_{i,l} d_il * ksk_b[i,l][0], with the
 //                  reference's u64-wrapping digit * key products, its `digit
 //                  == 0` skip and its raw (unreduced) body when every digit

@@ -785,7 +785,7 @@ class BootstrapEngine:
 
     @staticmethod
     def key_switch(q: int, base_log: int, level: int, ksk_a, ksk_b, lwe_a, lwe_b, device: int = 0):
-        """key_switch (:630-677): ksk_a [in_dim*level, out_dim], ksk_b
+        """key_switch (:626-674): ksk_a [in_dim*level, out_dim], ksk_b
         [in_dim*level]; lwe_a [..., in_dim], lwe_b [...] -> (a, b)."""
         ksk_a, ksk_b, lwe_a, lwe_b = (_as_u64(x) for x in (ksk_a, ksk_b, lwe_a, lwe_b))
         in_dim = int(lwe_a.shape[-1])

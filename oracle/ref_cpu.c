@@ -591,7 +591,7 @@ void oracle_blind_rotate(const oracle_ntt *t, u32 k, u32 base_log, u32 level, u3
     free(rot); free(res);
 }
 
-/* key_switch (:630-677): ksk_a [in_dim*level][out_dim] (keys[idx].first),
+/* key_switch (:626-674): ksk_a [in_dim*level][out_dim] (keys[idx].first),
  * ksk_b [in_dim*level] (keys[idx].second[0]). */
 void oracle_key_switch(u64 q, u32 base_log, u32 level, u32 in_dim, u32 out_dim, const u64 *ksk_a,
                        const u64 *ksk_b, const u64 *lwe_a, u64 lwe_b, u64 *out_a, u64 *out_b) {

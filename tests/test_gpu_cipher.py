@@ -209,7 +209,7 @@ def test_key_switch_vs_oracle(fg, q, bl, lv):
 
 def test_bootstrap_pipeline_device(fg):
     """blind_rotate -> sample_extract -> key_switch on device tensors equals
-    the oracle's bootstrap_with_test_poly sequence (:679-708)."""
+    the oracle's bootstrap_with_test_poly sequence (:676-708)."""
     import torch
 
     n, q, bl, lv, dim, k, b = 512, 12289, 4, 3, 8, 1, 4

@@ -2,7 +2,7 @@
 oracle_ct_multiply, oracle_relinearize, oracle_cmux, oracle_blind_rotate,
 oracle_key_switch) against a second, independently written pure-Python
 restatement of the reference code (encryption.cpp:737-980,
-bootstrap_engine.cpp:122-145, 520-677) built on ``oracle.pyref``'s big-integer
+bootstrap_engine.cpp:122-145, 520-674) built on ``oracle.pyref``'s big-integer
 transform, plus the committed golden vectors.  No GPU needed.
 """
 import json
@@ -135,7 +135,7 @@ def py_blind_rotate(acc, lwe_a, lwe_b, bsk, q, bl, lv, k=1):  # :547-577
     return acc
 
 
-def py_key_switch(q, bl, lv, ksk_a, ksk_b, lwe_a, lwe_b):  # :630-677
+def py_key_switch(q, bl, lv, ksk_a, ksk_b, lwe_a, lwe_b):  # :626-674
     out_dim = ksk_a.shape[1]
     ra = [0] * out_dim
     rb = lwe_b
