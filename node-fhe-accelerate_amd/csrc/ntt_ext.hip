@@ -59,7 +59,11 @@ constexpr int ext_stash() {
     // relinearisation (MODE 1): accumulator 0 in LDS, accumulator 1 and the
     // c2 words in VGPRs (one workgroup per CU); c2 is then read once instead
     // of once per digit level
-    if (MODE == 1 && K1 == 2 && G::P == 1 && (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024) return 3;
+#ifndef FHE_RELIN_REGS
+#define FHE_RELIN_REGS 1
+#endif
+    if (FHE_RELIN_REGS && MODE == 1 && K1 == 2 && G::P == 1 && (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024)
+        return 3;
     return 2;
 }
 template <int LOGN, typename W, int K1, int MODE = 0>
