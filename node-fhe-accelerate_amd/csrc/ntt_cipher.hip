@@ -30,9 +30,15 @@
 namespace FHE_NS {
 
 // Slots held in LDS: 3 (all), 1 (C only; A, B in HBM rows) or 0 (C in VGPRs).
+#ifndef FHE_CTMUL_PREFER_REGS
+#define FHE_CTMUL_PREFER_REGS 1
+#endif
 template <int LOGN, typename W>
 constexpr int ctmul_lds_slots() {
     using G = Geo<LOGN>;
+    // slots A/B in VGPRs and C in LDS keeps more workgroups resident than all
+    // three in LDS (e.g. N=8192/u32: 2 workgroups per CU instead of 1)
+    if (FHE_CTMUL_PREFER_REGS && G::P == 1 && (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024) return 1;
     if (G::P * (G::LW + 3 * G::N) * (int)sizeof(W) <= 160 * 1024) return 3;
     if (G::P * (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024) return 1;
     return 0;
