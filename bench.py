@@ -53,19 +53,47 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N fresh
+    rank processes under torch.distributed.run (one per GPU) as CHILDREN of
+    this process and return their exit code.  Called before anything touches
+    the GPU; the parent never re-execs itself.  Rank 0 prints the JSON line."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; FHE_DIST_BACKEND=gloo (+ several ranks per GPU)
-    # exercises the multi-rank path on a single-GPU box
-    dev = local % max(1, torch.cuda.device_count())
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # one process per GPU.  More ranks than devices (rehearsing N ranks on a
+    # one-GPU box) share devices round-robin and need FHE_DIST_BACKEND=gloo:
+    # RCCL refuses two ranks on one GPU.
+    ndev = max(1, torch.cuda.device_count())
+    dev = local % ndev
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("FHE_DIST_BACKEND", "nccl")
+        backend = os.environ.get("FHE_DIST_BACKEND", "nccl" if world <= ndev else "gloo")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -124,6 +152,8 @@ def gpu_workload(fhe_gpu, n, q, batch, steps, warmup, dist, only="", check=True)
         res["fwd"] = timed(dist, lambda: ring.forward_ntt(a, out=out), steps, warmup)
     if only == "inv":
         res["inv"] = timed(dist, lambda: ring.inverse_ntt(a, out=out), steps, warmup)
+    if dist is not None and only in ("", "fwd_mul"):
+        res["gather"] = time_gather(dist, out, n)
     # spot-check a few rows bit-exactly against the oracle (outside timing)
     if not check:
         res["parity_ok"] = "skipped"
@@ -132,6 +162,30 @@ def gpu_workload(fhe_gpu, n, q, batch, steps, warmup, dist, only="", check=True)
     del a, b, out
     torch.cuda.empty_cache()
     return res
+
+
+def time_gather(dist, out, n, polys=4096):
+    """the optional result gather to rank 0 (RCCL over xGMI
+    with the nccl backend), timed on its own and never part of `value`:
+    `polys` result polynomials per rank (512 MiB at N=16384) gathered into
+    rank 0."""
+    from fhe_gpu.shard import gather_to_root
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    g = min(polys, out.shape[0])
+    local = out[:g]
+    if dist.get_backend() != "nccl":
+        local = local.cpu()  # gloo gathers host tensors
+    gather_to_root(local, g * world, rank, world)  # warm-up (communicator setup)
+    barrier(dist)
+    t0 = time.perf_counter()
+    full = gather_to_root(local, g * world, rank, world)
+    barrier(dist)
+    ms = max_over_ranks(dist, (time.perf_counter() - t0) * 1e3)
+    del full
+    nbytes = g * n * 8 * world
+    return {"backend": dist.get_backend(), "polys_per_rank": g, "bytes_into_root": nbytes, "ms": ms,
+            "GBps_into_root": nbytes / (ms * 1e-3) / 1e9}
 
 
 def _spot_check(ring, a, b, out, n, q, batch):
@@ -249,34 +303,66 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
     return res
 
 
+KERNEL_SYMBOL = {"fwd_mul": "k_ntt_fwd_mul", "polymul": "k_polymul", "fwd": "k_ntt_fwd", "inv": "k_ntt_inv"}
+
+
 def pmc_traffic(kernel, n, batch, q):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of the
-    same workload (profiles/*/summary.json, tools/summarize_profile.py)."""
+    same workload (profiles/*/summary.json, tools/summarize_profile.py).
+    Only summaries whose profiled kernel is the template this run launches
+    (`k_<name><logN, word type`) count; among those the newest `generated`
+    stamp wins (summaries without one rank below every stamped one)."""
     import glob
 
+    logn = n.bit_length() - 1
+    sym = f"{KERNEL_SYMBOL[kernel]}<{logn}, {'unsigned int' if q < (1 << 30) else 'unsigned long'},"
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json"))):
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
         try:
             s = json.load(open(f))
         except Exception:
             continue
         w = s.get("workload", {})
-        if (w.get("kernel") == kernel and w.get("n") == n and w.get("batch") == batch and w.get("q") == q
-                and "hbm_traffic_bytes_per_launch" in s):
-            best = (s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
-    return best
+        if not (w.get("kernel") == kernel and w.get("n") == n and w.get("batch") == batch and w.get("q") == q
+                and "hbm_traffic_bytes_per_launch" in s and sym in s.get("kernel_name", "")):
+            continue
+        key = (s.get("generated", ""), f)
+        if best is None or key > best[0]:
+            best = (key, s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best[1:] if best else None
+
+
+def host_info():
+    """Host CPU facts for the cpu_baseline record."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
 
 
 def cpu_baseline(n, q, seconds, threads=None):
     """The oracle (C restatement of the reference NTTProcessor + pointwise,
-    same % -based op sequence) on the host cores, bounded sample."""
+    same % -based op sequence) on the host cores, bounded sample.  Threads:
+    every core this process may run on, capped by OMP_NUM_THREADS when the
+    host sets one (the GPU box sets it to the job's CPU share: its affinity
+    mask lists the whole machine, shared with other jobs)."""
     import oracle
 
+    info = host_info()
     if threads is None:
-        try:
-            threads = min(16, len(os.sched_getaffinity(0)))
-        except Exception:
-            threads = 8
+        threads = info["affinity_cpus"]
+        omp = os.environ.get("OMP_NUM_THREADS", "")
+        if omp.isdigit() and int(omp) > 0:
+            threads = min(threads, int(omp))
     t = oracle.NTT(n, q)
     chunk = threads * 2
     a = oracle.splitmix_fill(1, q, chunk * n).reshape(chunk, n)
@@ -290,12 +376,17 @@ def cpu_baseline(n, q, seconds, threads=None):
         if el >= seconds:
             break
     return {"value": done / el, "unit": "NTTs/s", "cores": threads, "kind": "port",
+            "calibration": "uncalibrated port: the reference C++ is not buildable here (modular_arithmetic.h "
+                           "includes <arm_neon.h>), so the +-10% calibration of BASELINE.md section 2 was not possible",
+            **info,
             "sample": f"{done} x (forward NTT + pointwise modmul), N={n}, q={q}, {threads} threads, {el:.1f}s; "
                       f"oracle/ref_cpu.c restatement of NTTProcessor::forward_ntt + pointwise_multiply"}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     dist, rank, world, local = dist_setup(args)
     import fhe_gpu
 
@@ -333,6 +424,8 @@ def main():
         "value": value,
         "unit": "NTTs/s",
         "n_gpus": world,
+        "ranks_seen": dist.get_world_size() if dist is not None else 1,
+        "devices_used": len({(r % max(1, torch.cuda.device_count())) for r in range(world)}),
         "steps": K,
         "warmup": W,
         "ms_per_step": wall / K * 1e3,
@@ -355,6 +448,8 @@ def main():
         line["roofline"]["traffic"] = tr[0]
         line["roofline"]["traffic_source"] = tr[1]
         line["roofline"]["traffic_over_algorithmic"] = tr[0] / (bytes_per_unit * B)
+    if "gather" in r:
+        line["gather"] = r["gather"]
     if "polymul" in r:
         pw, pk = r["polymul"]
         line["polymuls_per_s"] = world * B * K / pw

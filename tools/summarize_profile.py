@@ -26,7 +26,10 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     ksub = sys.argv[sys.argv.index("--kernel-substr") + 1] if "--kernel-substr" in sys.argv else "fwd_mul"
     os.makedirs(dst, exist_ok=True)
-    out = {"source": src, "kernel_substr": ksub}
+    import datetime
+
+    out = {"source": src, "kernel_substr": ksub,
+           "generated": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
     if "--workload" in sys.argv:
         k, n, b, q = sys.argv[sys.argv.index("--workload") + 1].split(",")
         out["workload"] = {"kernel": k, "n": int(n), "batch": int(b), "q": int(q)}
