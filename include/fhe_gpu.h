@@ -87,6 +87,25 @@ int fhe_detect(fhe_hw_caps *caps);
  * device: HIP device ordinal.                                              */
 int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out);
 void fhe_ctx_destroy(fhe_ctx *ctx);
+/* Multi-device context (SURVEY.md 8(b) `devices, ndev`): one transform
+ * context per listed device (tables, scratch and stream replicated; a
+ * device may be listed twice).  Every batch entry point below accepts it:
+ *   FHE_HOST    the batch is cut into ndev contiguous balanced ranges, each
+ *               staged through its own device by its own host thread (the
+ *               reference's batch_encrypt chunks a batch over threads sharing
+ *               one read-only NTTProcessor, encryption.cpp:472, 520-533);
+ *               returns when every range is back in host memory;
+ *   FHE_DEVICE  the pointers are device memory of one listed device and the
+ *               call runs there (data stays where it lives; shard across
+ *               devices by calling once per device-resident shard).
+ * Key preparation (fhe_ggsw_prepare, fhe_relin_key_prepare, fhe_secret_key_prepare,
+ * fhe_public_key_prepare) runs on the first device for FHE_HOST.
+ * fhe_ctx_set_stream binds the stream to the sub-context of its device.     */
+int fhe_ctx_create_multi(uint32_t n, uint64_t q, int mode, const int *devices, int ndev, fhe_ctx **out);
+int fhe_ctx_device_count(const fhe_ctx *ctx, int *ndev);
+/* The per-device context i (borrowed; owned by ctx).  A single-device
+ * context returns itself for i = 0. */
+int fhe_ctx_sub(const fhe_ctx *ctx, int i, fhe_ctx **out);
 /* Enqueue all later work of this context on the given hipStream_t (e.g. the
  * caller's torch stream).  NULL selects the null (legacy default) stream,
  * which is torch's default stream.  A new context uses a private

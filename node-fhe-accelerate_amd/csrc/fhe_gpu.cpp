@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -113,6 +114,15 @@ struct fhe_ctx {
     std::mutex br_mu;
     void *br_tmp = nullptr;
     size_t br_tmp_bytes = 0;
+    // completion of the last enqueued use of br_tmp: a call on another
+    // stream waits for it before reusing the buffer
+    hipEvent_t br_done = nullptr;
+    hipStream_t br_done_stream = nullptr;
+    // multi-device context (fhe_ctx_create_multi): one full context per
+    // listed device; this object then only holds the parameters and routes
+    // every call to them
+    std::vector<fhe_ctx *> subs;
+    bool multi() const { return !subs.empty(); }
 };
 
 namespace {
@@ -211,6 +221,7 @@ void free_tables(fhe_ctx *c) {
     c->br = fhe_ctx::BrGraph{};
     if (c->br_tmp) { (void)hipFree(c->br_tmp); c->br_tmp = nullptr; }
     c->br_tmp_bytes = 0;
+    if (c->br_done) { (void)hipEventDestroy(c->br_done); c->br_done = nullptr; }
 }
 
 FHE_NS::ModConsts mod_consts(u64 q) {
@@ -230,6 +241,78 @@ int check_ctx(const fhe_ctx *c) {
     if (!c) return fail(FHE_ERR_INVALID_ARG, "null context");
     return FHE_OK;
 }
+
+// ---------------------------------------------------------------- multi-device routing
+// The sub-context that owns device buffer p (FHE_DEVICE calls run where
+// their data lives).
+fhe_ctx *sub_for_pointer(const fhe_ctx *m, const void *p) {
+    hipPointerAttribute_t at{};
+    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    for (fhe_ctx *s : m->subs)
+        if (s->device == at.device) return s;
+    return nullptr;
+}
+
+// Run fn(sub, lo, count) over a multi-device context.  FHE_HOST: the batch
+// is cut into ndev contiguous balanced ranges (fhe_gpu/shard.py's
+// shard_range), one host thread per device (the last range on the calling
+// thread), as the reference's batch_encrypt chunks a batch over threads that
+// share one read-only NTTProcessor (encryption.cpp:472, 520-533).
+// FHE_DEVICE: the whole batch on the sub-context of the device that holds
+// `probe`.
+template <typename F>
+int multi_run(fhe_ctx *m, size_t batch, int where, const void *probe, F &&fn) {
+    if (where != FHE_HOST && where != FHE_DEVICE) return fail(FHE_ERR_INVALID_ARG, "where must be FHE_HOST or FHE_DEVICE");
+    if (batch == 0) return FHE_OK;
+    if (where == FHE_DEVICE) {
+        fhe_ctx *s = sub_for_pointer(m, probe);
+        if (!s) return fail(FHE_ERR_INVALID_ARG, "device buffer is not memory of any device of this context");
+        return fn(s, (size_t)0, batch);
+    }
+    const size_t nd = m->subs.size(), base = batch / nd, extra = batch % nd;
+    std::vector<int> rc(nd, FHE_OK);
+    std::vector<std::string> msg(nd);
+    std::vector<std::thread> th;
+    size_t lo = 0;
+    for (size_t i = 0; i < nd; ++i) {
+        const size_t cnt = base + (i < extra ? 1 : 0);
+        if (cnt) {
+            auto job = [&, i, lo, cnt] {
+                rc[i] = fn(m->subs[i], lo, cnt);
+                if (rc[i] != FHE_OK) msg[i] = g_err;
+            };
+            if (i + 1 == nd) job();
+            else th.emplace_back(job);
+        }
+        lo += cnt;
+    }
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < nd; ++i)
+        if (rc[i] != FHE_OK) return fail(rc[i], msg[i]);
+    return FHE_OK;
+}
+// Whole-call routing for the single-buffer entry points (key preparation):
+// the device of `probe` (FHE_DEVICE) or the first device (FHE_HOST).
+template <typename F>
+int multi_one(fhe_ctx *m, int where, const void *probe, F &&fn) {
+    if (where == FHE_DEVICE) {
+        fhe_ctx *s = sub_for_pointer(m, probe);
+        if (!s) return fail(FHE_ERR_INVALID_ARG, "device buffer is not memory of any device of this context");
+        return fn(s);
+    }
+    return fn(m->subs[0]);
+}
+// Route a batch entry point of a multi-device context: CALL runs with `c`
+// bound to the sub-context and [lo, lo + nb) its range of the batch.
+#define FHE_MULTI(BATCH, WHERE, PROBE, CALL)                                                           \
+    if (c && c->multi())                                                                               \
+    return multi_run(c, (BATCH), (WHERE), (PROBE),                                                     \
+                     [&](fhe_ctx *sub, size_t lo, size_t nb) { return [&](fhe_ctx *c) { return CALL; }(sub); })
+#define FHE_MULTI_ONE(WHERE, PROBE, CALL) \
+    if (c && c->multi()) return multi_one(c, (WHERE), (PROBE), [&](fhe_ctx *sub) { return [&](fhe_ctx *c) { return CALL; }(sub); })
 
 // Host staging: run fn(device pointers) over chunks of at most `chunk` polys.
 // nin inputs, one output; all of n*batch u64 per buffer (or `elems` each).
@@ -484,8 +567,53 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     return FHE_OK;
 }
 
+int fhe_ctx_create_multi(uint32_t n, uint64_t q, int mode, const int *devices, int ndev, fhe_ctx **out) {
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    if (!devices || ndev < 1) return fail(FHE_ERR_INVALID_ARG, "at least one device required");
+    fhe_ctx *m = new fhe_ctx();
+    for (int i = 0; i < ndev; ++i) {
+        fhe_ctx *s = nullptr;
+        const int rc = fhe_ctx_create(n, q, mode, devices[i], &s);
+        if (rc != FHE_OK) {
+            const std::string msg = g_err;
+            fhe_ctx_destroy(m);
+            return fail(rc, msg);
+        }
+        m->subs.push_back(s);
+    }
+    const fhe_ctx *s0 = m->subs[0];
+    m->n = s0->n; m->logn = s0->logn; m->q = s0->q; m->psi = s0->psi; m->psi_inv = s0->psi_inv;
+    m->inv_n = s0->inv_n; m->mode = s0->mode; m->device = s0->device; m->word = s0->word;
+    m->fwd_tw = s0->fwd_tw; m->inv_tw = s0->inv_tw;
+    m->stream = s0->stream;
+    *out = m;
+    return FHE_OK;
+}
+
+int fhe_ctx_device_count(const fhe_ctx *c, int *ndev) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!ndev) return fail(FHE_ERR_INVALID_ARG, "null out");
+    *ndev = c->multi() ? (int)c->subs.size() : 1;
+    return FHE_OK;
+}
+
+int fhe_ctx_sub(const fhe_ctx *c, int i, fhe_ctx **out) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null out");
+    const int nd = c->multi() ? (int)c->subs.size() : 1;
+    if (i < 0 || i >= nd) return fail(FHE_ERR_INVALID_ARG, "device index out of range");
+    *out = c->multi() ? c->subs[i] : const_cast<fhe_ctx *>(c);
+    return FHE_OK;
+}
+
 void fhe_ctx_destroy(fhe_ctx *c) {
     if (!c) return;
+    if (c->multi()) {
+        for (auto it = c->subs.rbegin(); it != c->subs.rend(); ++it) fhe_ctx_destroy(*it);
+        delete c;
+        return;
+    }
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_tables(c);
@@ -495,6 +623,18 @@ void fhe_ctx_destroy(fhe_ctx *c) {
 
 int fhe_ctx_set_stream(fhe_ctx *c, void *s) {
     if (int rc = check_ctx(c)) return rc;
+    if (c->multi()) {  // the sub-context(s) of the stream's device
+        int dev = -1;
+        HIP_TRY(s ? hipStreamGetDevice((hipStream_t)s, &dev) : hipGetDevice(&dev), "hipStreamGetDevice");
+        bool hit = false;
+        for (fhe_ctx *sub : c->subs)
+            if (sub->device == dev) {
+                fhe_ctx_set_stream(sub, s);
+                hit = true;
+            }
+        if (!hit) return fail(FHE_ERR_INVALID_ARG, "stream is not on any device of this context");
+        return FHE_OK;
+    }
     c->stream = (hipStream_t)s;  // NULL is the device's null (legacy default) stream
     c->plan.stream = c->stream;
     return FHE_OK;
@@ -502,6 +642,11 @@ int fhe_ctx_set_stream(fhe_ctx *c, void *s) {
 void *fhe_ctx_stream(const fhe_ctx *c) { return c ? (void *)c->stream : nullptr; }
 int fhe_ctx_synchronize(fhe_ctx *c) {
     if (int rc = check_ctx(c)) return rc;
+    if (c->multi()) {
+        for (fhe_ctx *sub : c->subs)
+            if (int rc = fhe_ctx_synchronize(sub)) return rc;
+        return FHE_OK;
+    }
     DeviceGuard g(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     return FHE_OK;
@@ -527,16 +672,19 @@ int fhe_ctx_get_twiddles(const fhe_ctx *c, uint64_t *fwd, uint64_t *inv) {
 }
 
 int fhe_ntt_fwd_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, in, fhe_ntt_fwd_batch(c, in + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
                        [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 0); });
 }
 int fhe_ntt_inv_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, in, fhe_ntt_inv_batch(c, in + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
                        [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_inv(c->plan, d[0], o, nb); });
 }
 int fhe_ntt_fwd_mul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, a, fhe_ntt_fwd_mul_batch(c, a + lo * c->n, w + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!w && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     return run_poly_op(c, a, w, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
@@ -544,6 +692,7 @@ int fhe_ntt_fwd_mul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *w, uint
     });
 }
 int fhe_polymul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, a, fhe_polymul_batch(c, a + lo * c->n, b + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
@@ -551,6 +700,7 @@ int fhe_polymul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t
     });
 }
 int fhe_pointwise_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, a, fhe_pointwise_batch(c, a + lo * c->n, b + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const FHE_NS::ModConsts m = mod_consts(c->q);
@@ -559,6 +709,7 @@ int fhe_pointwise_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64
     });
 }
 int fhe_poly_add_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, a, fhe_poly_add_batch(c, a + lo * c->n, b + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const FHE_NS::ModConsts m = mod_consts(c->q);
@@ -567,6 +718,7 @@ int fhe_poly_add_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_
     });
 }
 int fhe_poly_sub_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, a, fhe_poly_sub_batch(c, a + lo * c->n, b + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const FHE_NS::ModConsts m = mod_consts(c->q);
@@ -575,6 +727,7 @@ int fhe_poly_sub_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_
     });
 }
 int fhe_poly_neg_batch(fhe_ctx *c, const uint64_t *a, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, a, fhe_poly_neg_batch(c, a + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
         return FHE_NS::launch_neg(c->q, d[0], o, nb * c->n, c->stream);
@@ -582,6 +735,7 @@ int fhe_poly_neg_batch(fhe_ctx *c, const uint64_t *a, uint64_t *out, size_t batc
 }
 int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, uint64_t *out, size_t batch,
                               int where) {
+    FHE_MULTI(batch, where, a, fhe_poly_mul_scalar_batch(c, a + lo * c->n, scalar, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     const FHE_NS::ModConsts m = mod_consts(c->q);
     const u64 s = scalar % c->q;
@@ -601,6 +755,7 @@ static int check_decomp(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_
 }
 
 int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggsw, uint64_t *ggsw_ntt, int where) {
+    FHE_MULTI_ONE(where, ggsw, fhe_ggsw_prepare(c, k, level, ggsw, ggsw_ntt, where));
     if (int rc = check_ctx(c)) return rc;
     if ((int)c->logn > FHE_NS::kMaxFusedLogN)
         return fail(FHE_ERR_UNSUPPORTED, "external product implemented for degrees up to 16384");
@@ -613,6 +768,7 @@ int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggs
 
 int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
                                const uint64_t *ggsw_ntt, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, glwe, fhe_external_product_batch(c, k, base_log, level, glwe + lo * (k + 1) * c->n, ggsw_ntt, out + lo * (k + 1) * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (int rc = check_decomp(c, k, base_log, level)) return rc;
     if (!ggsw_ntt && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
@@ -639,6 +795,7 @@ int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32
 
 int fhe_decompose_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *poly, uint64_t *out,
                         size_t npoly, int where) {
+    FHE_MULTI(npoly, where, poly, fhe_decompose_batch(c, base_log, level, poly + lo * c->n, out + lo * (size_t)level * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
         return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
@@ -652,6 +809,7 @@ int fhe_decompose_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uin
 
 int fhe_ct_multiply_batch(fhe_ctx *c, const uint64_t *ct1, const uint64_t *ct2, uint64_t *out, size_t batch,
                           int is_ntt, int where) {
+    FHE_MULTI(batch, where, ct1, fhe_ct_multiply_batch(c, ct1 + lo * 2 * c->n, ct2 + lo * 2 * c->n, out + lo * 3 * c->n, nb, is_ntt, where));
     FHE_TRY(check_common(c, where, batch));
     if (batch == 0) return FHE_OK;
     if (!ct1 || !ct2 || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
@@ -666,6 +824,7 @@ int fhe_ct_multiply_batch(fhe_ctx *c, const uint64_t *ct1, const uint64_t *ct2, 
 }
 
 int fhe_relin_key_prepare(fhe_ctx *c, uint32_t level, const uint64_t *rlk, uint64_t *rlk_ntt, int where) {
+    FHE_MULTI_ONE(where, rlk, fhe_relin_key_prepare(c, level, rlk, rlk_ntt, where));
     if (int rc = check_ctx(c)) return rc;
     FHE_TRY(check_fused(c, "relinearisation"));
     return run_poly_op(c, rlk, nullptr, rlk_ntt, (size_t)2 * level, where, c->n, c->n,
@@ -674,6 +833,7 @@ int fhe_relin_key_prepare(fhe_ctx *c, uint32_t level, const uint64_t *rlk, uint6
 
 int fhe_relinearize_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *ct3,
                           const uint64_t *rlk_ntt, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, ct3, fhe_relinearize_batch(c, base_log, level, ct3 + lo * 3 * c->n, rlk_ntt, out + lo * 2 * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
     FHE_TRY(check_fused(c, "relinearisation"));
     FHE_TRY(check_relin_decomp(base_log, level));
@@ -692,6 +852,7 @@ int fhe_relinearize_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const u
 int fhe_ct_multiply_relin_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *ct1,
                                 const uint64_t *ct2, const uint64_t *rlk_ntt, uint64_t *out, size_t batch,
                                 int where) {
+    FHE_MULTI(batch, where, ct1, fhe_ct_multiply_relin_batch(c, base_log, level, ct1 + lo * 2 * c->n, ct2 + lo * 2 * c->n, rlk_ntt, out + lo * 2 * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
     FHE_TRY(check_fused(c, "relinearisation"));
     FHE_TRY(check_relin_decomp(base_log, level));
@@ -795,6 +956,7 @@ static int check_tfhe(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t 
 
 int fhe_glwe_rotate_batch(fhe_ctx *c, uint32_t k, const int32_t *rot, const uint64_t *glwe, uint64_t *out,
                           size_t batch, int where) {
+    FHE_MULTI(batch, where, glwe, fhe_glwe_rotate_batch(c, k, rot + lo, glwe + lo * (k + 1) * c->n, out + lo * (k + 1) * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
     if (batch == 0) return FHE_OK;
     if (!rot || !glwe || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
@@ -812,6 +974,7 @@ int fhe_glwe_rotate_batch(fhe_ctx *c, uint32_t k, const int32_t *rot, const uint
 
 int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *ggsw_ntt,
                    const uint64_t *ct0, const uint64_t *ct1, uint64_t *out, size_t batch, int where) {
+    FHE_MULTI(batch, where, ct0, fhe_cmux_batch(c, k, base_log, level, ggsw_ntt, ct0 + lo * (k + 1) * c->n, ct1 + lo * (k + 1) * c->n, out + lo * (k + 1) * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
     FHE_TRY(check_tfhe(c, k, base_log, level));
     if (batch == 0) return FHE_OK;
@@ -833,6 +996,7 @@ int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, co
 int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
                            const uint64_t *lwe_a, const uint64_t *lwe_b, uint64_t lwe_q, const uint64_t *bsk_ntt,
                            uint64_t *acc, size_t batch, int where) {
+    FHE_MULTI(batch, where, acc, fhe_blind_rotate_batch(c, k, base_log, level, lwe_dim, lwe_a + lo * lwe_dim, lwe_b + lo, lwe_q, bsk_ntt, acc + lo * (k + 1) * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
     FHE_TRY(check_tfhe(c, k, base_log, level));
     if (lwe_q == 0) return fail(FHE_ERR_ZERO_MODULUS, "LWE modulus must be non-zero");
@@ -857,6 +1021,9 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
         c->br_tmp_bytes = bytes;
     }
     u64 *tmp = (u64 *)c->br_tmp;
+    // br_tmp may still be in use by a call enqueued on another stream
+    if (c->br_done && c->br_done_stream != c->stream)
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->br_done, 0), "hipStreamWaitEvent");
     // acc <- X^-round(b 2N / q) acc, into tmp; then lwe_dim CMux steps
     // ping-ponging tmp <-> acc; the result is copied back into acc if it
     // ended in tmp.
@@ -910,11 +1077,15 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
         e = enqueue();
     }
     if (e != hipSuccess) return hip_fail(e, "blind rotate");
+    if (!c->br_done) HIP_TRY(hipEventCreateWithFlags(&c->br_done, hipEventDisableTiming), "hipEventCreate");
+    HIP_TRY(hipEventRecord(c->br_done, c->stream), "hipEventRecord");
+    c->br_done_stream = c->stream;
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 
 int fhe_sample_extract_batch(fhe_ctx *c, uint32_t k, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
                              size_t batch, int where) {
+    FHE_MULTI(batch, where, glwe, fhe_sample_extract_batch(c, k, glwe + lo * (k + 1) * c->n, lwe_a + lo * k * c->n, lwe_b + lo, nb, where));
     FHE_TRY(check_common(c, where, batch));
     if (batch == 0) return FHE_OK;
     if (!glwe || !lwe_b || (k && !lwe_a)) return fail(FHE_ERR_INVALID_ARG, "null buffer");

@@ -69,7 +69,11 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 #ifndef FHE_CTMUL_AREG
 #define FHE_CTMUL_AREG 1
 #endif
-    constexpr bool AREG = NL == 1 && FHE_CTMUL_AREG;
+    // (u64: only where the VGPR slots fit without scratch spills -- at N =
+    // 4096/8192 they took 255 VGPRs plus scratch, and the N = 8192
+    // negacyclic build faulted on MI355X; the HBM-row slots with prefetch
+    // need 167-241 VGPRs and no scratch)
+    constexpr bool AREG = NL == 1 && FHE_CTMUL_AREG && sizeof(W) == 4;
     W areg[AREG ? G::E : 1];
     W breg[AREG ? G::E : 1];
     // HBM slots (NL < 3) hold W words in the first half of their u64 row

@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 from typing import Optional
 
 import numpy as np
@@ -94,6 +95,9 @@ SIGNATURES = [
     ("fhe_detect", C.c_int, [C.POINTER(HwCaps)]),
     ("fhe_ctx_create", C.c_int, [C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.POINTER(vp)]),
     ("fhe_ctx_destroy", None, [vp]),
+    ("fhe_ctx_create_multi", C.c_int, [C.c_uint32, C.c_uint64, C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
+    ("fhe_ctx_device_count", C.c_int, [vp, C.POINTER(C.c_int)]),
+    ("fhe_ctx_sub", C.c_int, [vp, C.c_int, C.POINTER(vp)]),
     ("fhe_ctx_set_stream", C.c_int, [vp, vp]),
     ("fhe_ctx_stream", vp, [vp]),
     ("fhe_ctx_synchronize", C.c_int, [vp]),
@@ -197,14 +201,14 @@ def _is_tensor(x) -> bool:
     return _HAVE_TORCH and isinstance(x, torch.Tensor)
 
 
-def _stream_ptr():
-    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+def _stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
 class _Buf:
     """Pointer + placement for one argument."""
 
-    __slots__ = ("ptr", "where", "count", "keep")
+    __slots__ = ("ptr", "where", "count", "keep", "device")
 
     def __init__(self, x, writable=False):
         if _is_tensor(x):
@@ -215,6 +219,7 @@ class _Buf:
             if not x.is_contiguous():
                 raise FHEError(-9, "device buffers must be contiguous")
             self.ptr, self.where, self.count, self.keep = x.data_ptr(), FHE_DEVICE, x.numel(), x
+            self.device = x.device
         else:
             a = x
             if not (isinstance(a, np.ndarray) and a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]):
@@ -222,12 +227,20 @@ class _Buf:
                     raise FHEError(-9, "output must be a C-contiguous numpy uint64 array")
                 a = np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
             self.ptr, self.where, self.count, self.keep = a.ctypes.data, FHE_HOST, a.size, a
+            self.device = None
+
+
+_TLS = threading.local()  # device of the last _where() call's tensors (for _bind_stream)
 
 
 def _where(*bufs: _Buf) -> int:
     w = {b.where for b in bufs if b is not None}
     if len(w) != 1:
         raise FHEError(-9, "all buffers of one call must be host arrays or all device tensors")
+    devs = {b.device for b in bufs if b is not None and b.device is not None}
+    if len(devs) > 1:
+        raise FHEError(-9, "all device tensors of one call must be on the same GPU")
+    _TLS.device = devs.pop() if devs else None
     return w.pop()
 
 
@@ -304,13 +317,23 @@ class NTTProcessor:
     mod_inverse = staticmethod(mod_inverse)
     find_primitive_root = staticmethod(find_primitive_root)
 
-    def __init__(self, degree: int, modulus: int, mode: str = "compat", device: int = 0):
+    def __init__(self, degree: int, modulus: int, mode: str = "compat", device: int = 0, devices=None):
+        """devices: a list of GPU ordinals for a multi-device context
+        (fhe_ctx_create_multi): host-array batches are split across them, a
+        device tensor runs on the GPU that holds it."""
         m = {"compat": MODE_COMPAT, "negacyclic": MODE_NEGACYCLIC}.get(mode)
         if m is None:
             raise FHEError(-9, f"unknown mode {mode!r}")
         h = C.c_void_p()
-        _check(lib().fhe_ctx_create(degree, modulus, m, device, C.byref(h)))
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            arr = (C.c_int * max(1, len(devs)))(*devs)
+            _check(lib().fhe_ctx_create_multi(degree, modulus, m, arr, len(devs), C.byref(h)))
+            device = devs[0]
+        else:
+            _check(lib().fhe_ctx_create(degree, modulus, m, device, C.byref(h)))
         self._h = h
+        self.devices = list(devices) if devices is not None else [device]
         self.degree, self.modulus, self.mode, self.device = degree, modulus, mode, device
         info = CtxInfo()
         _check(lib().fhe_ctx_get_info(h, C.byref(info)))
@@ -357,7 +380,7 @@ class NTTProcessor:
 
     def _bind_stream(self, where):
         if where == FHE_DEVICE:
-            _check(lib().fhe_ctx_set_stream(self._h, _stream_ptr()))
+            _check(lib().fhe_ctx_set_stream(self._h, _stream_ptr(getattr(_TLS, "device", None))))
 
     def _unary(self, fn, x, out):
         x = _as_u64(x)

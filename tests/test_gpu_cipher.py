@@ -33,8 +33,9 @@ def rnd(seed, q, *shape):
 
 
 # ------------------------------------------------------------ ciphertext multiply
+# (4096, P62) and (8192, P27) take the VGPR-slot layout (FHE_CTMUL_PREFER_REGS)
 @pytest.mark.parametrize("n,q", [(4, 17), (16, 97), (256, 7681), (1024, P27), (2048, P62), (4096, P27),
-                                 (8192, P62), (16384, P27), (16384, P62)])
+                                 (4096, P62), (8192, P27), (8192, P62), (16384, P27), (16384, P62)])
 def test_ct_multiply_vs_oracle(fg, n, q):
     b = 3 if n >= 8192 else 5
     r = fg.PolynomialRing(n, q)
@@ -77,7 +78,8 @@ def test_ct_multiply_negacyclic_is_ring_tensor(fg):
 
 
 @pytest.mark.parametrize("n,q,bl,lv", [(64, 257, 2, 4), (1024, P27, 4, 7), (1024, P27, 9, 3), (4096, P62, 16, 4),
-                                       (16384, P27, 4, 7), (16384, P62, 20, 3), (256, 7681, 63, 1)])
+                                       (8192, P62, 12, 5), (16384, P27, 4, 7), (16384, P62, 20, 3),
+                                       (256, 7681, 63, 1)])
 def test_relinearize_vs_oracle(fg, n, q, bl, lv):
     b = 2 if n >= 16384 else 4
     r = fg.PolynomialRing(n, q)
@@ -349,7 +351,7 @@ def test_ciphertext_linear_ops_and_plain(fg):
     assert (eng.relinearize(x, ek) == x).all()
 
 
-@pytest.mark.parametrize("n,q,bl,lv", [(16384, P27, 4, 7), (4096, P62, 16, 4)])
+@pytest.mark.parametrize("n,q,bl,lv", [(16384, P27, 4, 7), (8192, P27, 4, 7), (8192, P62, 13, 5), (4096, P62, 16, 4)])
 def test_decryption_identity_negacyclic(fg, n, q, bl, lv):
     """Size-independent property at full degree: in the negacyclic ring,
     noise-free ciphertexts ct_i = (m_i - a_i s, a_i) satisfy
