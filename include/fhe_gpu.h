@@ -229,6 +229,54 @@ int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t
                          const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a, const uint64_t *lwe_b,
                          uint64_t *out_a, uint64_t *out_b, size_t batch, int where, int device, void *hip_stream);
 
+/* ---- EncryptionEngine encrypt / decrypt / add_plain (encryption.cpp) ----
+ * The reference's RLWE encryption with its encoding: t = plaintext modulus
+ * (0 selects 4, encryption.cpp:40-46), delta = q / t, a plaintext is n slot
+ * values per ciphertext encoded as (v * delta mod 2^64) mod q
+ * (encode_packed :117-131; encode_plaintext is the one-slot case).
+ * fhe_secret_key_prepare  sk [n] (SecretKey::poly) -> sk_prep [2][n]
+ *   (NTT-domain s and s^2, Montgomery form; decrypt :256-271).
+ * fhe_public_key_prepare  pk [2][n] = (a, b) (PublicKey, key_manager.h:70-76)
+ *   -> pk_prep [2][n] (NTT-domain, Montgomery form).
+ * fhe_encrypt_batch  encrypt_internal (:171-205) with the sampled
+ *   polynomials supplied (u ternary, e1, e2 error; [batch][n] each, any u64
+ *   as x mod q), so the call is deterministic: ct [batch][2][n] =
+ *   (pk.b u + e1 + m, pk.a u + e2) under the context's transform product.
+ * fhe_decrypt_batch  decrypt / decrypt_packed (:234-348) of ciphertexts
+ *   [batch][components][n] (2: (c0, c1); 3: degree-2 (c0, c1, c2)); is_ntt
+ *   as Ciphertext::is_ntt.  Outputs (each nullable): values [batch][n] =
+ *   round(p t / q) mod t per coefficient of the phase p = c0 - c1 s
+ *   (- c2 s^2) (decode_packed :150-163; slot 0 is decode_plaintext),
+ *   phase [batch][n], max_noise [batch] = the integer whose double is the
+ *   reference's max_noise (compute_noise_budget :364-400); its noise
+ *   budget is log2(q / (2 max(max_noise, 1))), negative = the reference's
+ *   "Noise budget exhausted" failure.
+ * fhe_add_plain_batch  add_plain (:638-665): out = (c0 + m, c1), m
+ *   transformed first when is_ntt.
+ * Degrees up to 16384 (add_plain on coefficient-form ciphertexts: any). */
+int fhe_secret_key_prepare(fhe_ctx *ctx, const uint64_t *sk, uint64_t *sk_prep, int where);
+int fhe_public_key_prepare(fhe_ctx *ctx, const uint64_t *pk, uint64_t *pk_prep, int where);
+int fhe_encrypt_batch(fhe_ctx *ctx, uint64_t t, const uint64_t *pk_prep, const uint64_t *values, const uint64_t *u,
+                      const uint64_t *e1, const uint64_t *e2, uint64_t *ct, size_t batch, int where);
+int fhe_decrypt_batch(fhe_ctx *ctx, uint64_t t, const uint64_t *sk_prep, const uint64_t *ct, uint32_t components,
+                      int is_ntt, uint64_t *values, uint64_t *phase, uint64_t *max_noise, size_t batch, int where);
+int fhe_add_plain_batch(fhe_ctx *ctx, uint64_t t, const uint64_t *ct, const uint64_t *values, int is_ntt,
+                        uint64_t *out, size_t batch, int where);
+
+/* ---- BootstrapEngine::bootstrap_with_test_poly (bootstrap_engine.cpp:684-708)
+ * For each LWE ciphertext c (lwe_a [batch][lwe_dim], lwe_b [batch] mod
+ * lwe_q): acc = (0, .., 0, test_poly), blind_rotate (as
+ * fhe_blind_rotate_batch), sample_extract, then key_switch modulo the GLWE
+ * modulus with ksk_a [k*n*ks_level][out_dim], ksk_b [k*n*ks_level] (as
+ * fhe_key_switch_batch): out_a [batch][out_dim], out_b [batch].
+ * bootstrap() is the identity test polynomial; programmable_bootstrap
+ * (:716-722) passes a lookup table's polynomial. */
+int fhe_bootstrap_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
+                        const uint64_t *lwe_a, const uint64_t *lwe_b, uint64_t lwe_q, const uint64_t *bsk_ntt,
+                        const uint64_t *test_poly, uint32_t ks_base_log, uint32_t ks_level, uint32_t out_dim,
+                        const uint64_t *ksk_a, const uint64_t *ksk_b, uint64_t *out_a, uint64_t *out_b, size_t batch,
+                        int where);
+
 /* ---- context-free modular kernels --------------------------------------- */
 /* BarrettReducer::barrett_mul contract (modular_arithmetic.cpp:268-280):
  * c[i] = a[i]*b[i] mod q for any u64 inputs, any q != 0. stream may be NULL. */

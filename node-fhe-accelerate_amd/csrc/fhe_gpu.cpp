@@ -878,6 +878,141 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, c
     return rc;
 }
 
+// ---------------------------------------------------------------- EncryptionEngine encrypt / decrypt
+// Device temporaries of one call, stream-ordered (no device-wide sync).
+class StreamTemp {
+    std::vector<void *> p_;
+    hipStream_t s_;
+
+  public:
+    explicit StreamTemp(hipStream_t s) : s_(s) {}
+    ~StreamTemp() {
+        for (void *x : p_) (void)hipFreeAsync(x, s_);
+    }
+    int alloc(size_t bytes, u64 *&out) {
+        void *d = nullptr;
+        hipError_t e = hipMallocAsync(&d, bytes ? bytes : 8, s_);
+        if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMallocAsync: out of memory");
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+        p_.push_back(d);
+        out = (u64 *)d;
+        return FHE_OK;
+    }
+};
+
+int fhe_secret_key_prepare(fhe_ctx *c, const uint64_t *sk, uint64_t *sk_prep, int where) {
+    FHE_MULTI_ONE(where, sk, fhe_secret_key_prepare(c, sk, sk_prep, where));
+    FHE_TRY(check_common(c, where, 1));
+    FHE_TRY(check_fused(c, "encryption"));
+    if (!sk || !sk_prep) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, sk, n * 8, 1));
+    FHE_TRY(hs.map(where, sk_prep, 2 * n * 8, 2));
+    {
+        StreamTemp tmp(c->stream);
+        u64 *f = nullptr;
+        FHE_TRY(tmp.alloc(n * 8, f));
+        // row 0: fwd(s) R; row 1: fwd(s) * fwd(s) R (decrypt's sk^2, encryption.cpp:271)
+        HIP_TRY(FHE_NS::launch_fwd(c->plan, sk, f, 1, 0), "fwd kernel");
+        HIP_TRY(FHE_NS::launch_fwd(c->plan, sk, sk_prep, 1, 1), "fwd kernel");
+        HIP_TRY(FHE_NS::launch_modmul(mod_consts(c->q), f, sk_prep, sk_prep + n, n, c->stream), "modmul kernel");
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_public_key_prepare(fhe_ctx *c, const uint64_t *pk, uint64_t *pk_prep, int where) {
+    FHE_MULTI_ONE(where, pk, fhe_public_key_prepare(c, pk, pk_prep, where));
+    if (int rc = check_ctx(c)) return rc;
+    FHE_TRY(check_fused(c, "encryption"));
+    return run_poly_op(c, pk, nullptr, pk_prep, 2, where, c->n, c->n,
+                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 1); });
+}
+
+int fhe_encrypt_batch(fhe_ctx *c, uint64_t t, const uint64_t *pk_prep, const uint64_t *values, const uint64_t *u,
+                      const uint64_t *e1, const uint64_t *e2, uint64_t *ct, size_t batch, int where) {
+    FHE_MULTI(batch, where, ct, fhe_encrypt_batch(c, t, pk_prep, values + lo * c->n, u + lo * c->n, e1 + lo * c->n,
+                                                  e2 + lo * c->n, ct + lo * 2 * c->n, nb, where));
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_fused(c, "encryption"));
+    if (batch == 0) return FHE_OK;
+    if (!pk_prep || !values || !u || !e1 || !e2 || !ct) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, pk_prep, 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, values, batch * n * 8, 1));
+    FHE_TRY(hs.map(where, u, batch * n * 8, 1));
+    FHE_TRY(hs.map(where, e1, batch * n * 8, 1));
+    FHE_TRY(hs.map(where, e2, batch * n * 8, 1));
+    FHE_TRY(hs.map(where, ct, batch * 2 * n * 8, 2));
+    const u64 *ins[5] = {values, u, e1, e2, pk_prep};
+    for (const u64 *x : ins)
+        if (overlaps(ct, batch * 2 * n * 8, x, (x == pk_prep ? 2 : batch) * n * 8))
+            return fail(FHE_ERR_INVALID_ARG, "output must not overlap the inputs");
+    HIP_TRY(FHE_NS::launch_encrypt(c->plan, t, pk_prep, values, u, e1, e2, ct, batch), "encrypt kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_decrypt_batch(fhe_ctx *c, uint64_t t, const uint64_t *sk_prep, const uint64_t *ct, uint32_t components,
+                      int is_ntt, uint64_t *values, uint64_t *phase, uint64_t *max_noise, size_t batch, int where) {
+    FHE_MULTI(batch, where, ct, fhe_decrypt_batch(c, t, sk_prep, ct + lo * components * c->n, components, is_ntt,
+                                                  values ? values + lo * c->n : nullptr,
+                                                  phase ? phase + lo * c->n : nullptr,
+                                                  max_noise ? max_noise + lo : nullptr, nb, where));
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_fused(c, "decryption"));
+    if (components != 2 && components != 3) return fail(FHE_ERR_INVALID_ARG, "components must be 2 or 3");
+    if (batch == 0) return FHE_OK;
+    if (!sk_prep || !ct) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, sk_prep, 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, ct, batch * components * n * 8, 1));
+    FHE_TRY(hs.map(where, values, batch * n * 8, 2));
+    FHE_TRY(hs.map(where, phase, batch * n * 8, 2));
+    FHE_TRY(hs.map(where, max_noise, batch * 8, 2));
+    const size_t ctb = batch * components * n * 8;
+    if (overlaps(values, batch * n * 8, ct, ctb) || overlaps(phase, batch * n * 8, ct, ctb))
+        return fail(FHE_ERR_INVALID_ARG, "output must not overlap the ciphertexts");
+    int rc = FHE_OK;
+    {
+        StreamTemp tmp(c->stream);
+        u64 *ph = phase;
+        // degree-2 coefficient-form decryption keeps its partial phase in the phase row
+        if (!ph && components == 3 && !is_ntt) rc = tmp.alloc(batch * n * 8, ph);
+        if (rc == FHE_OK) {
+            hipError_t e = FHE_NS::launch_decrypt(c->plan, t, sk_prep, ct, (int)components, is_ntt, ph,
+                                                  phase != nullptr, values, max_noise, batch);
+            if (e != hipSuccess) rc = hip_fail(e, "decrypt kernel");
+        }
+    }
+    if (rc != FHE_OK) return rc;
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_add_plain_batch(fhe_ctx *c, uint64_t t, const uint64_t *ct, const uint64_t *values, int is_ntt, uint64_t *out,
+                        size_t batch, int where) {
+    FHE_MULTI(batch, where, ct, fhe_add_plain_batch(c, t, ct + lo * 2 * c->n, values + lo * c->n, is_ntt,
+                                                    out + lo * 2 * c->n, nb, where));
+    FHE_TRY(check_common(c, where, batch));
+    if (is_ntt) FHE_TRY(check_fused(c, "add_plain on NTT-domain ciphertexts"));
+    if (batch == 0) return FHE_OK;
+    if (!ct || !values || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, ct, batch * 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, values, batch * n * 8, 1));
+    FHE_TRY(hs.map(where, out, batch * 2 * n * 8, 2));
+    if (is_ntt && overlaps(out, batch * 2 * n * 8, values, batch * n * 8))
+        return fail(FHE_ERR_INVALID_ARG, "output must not overlap the plaintext");
+    HIP_TRY(FHE_NS::launch_add_plain(c->plan, t, ct, values, is_ntt, out, batch), "add_plain kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
 // ---------------------------------------------------------------- RNS ring
 struct fhe_rns_ctx {
     std::vector<fhe_ctx *> limbs;
@@ -1131,6 +1266,60 @@ int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t
     HIP_TRY(FHE_NS::launch_key_switch(mod_consts(q), base_log, level, in_dim, out_dim, ksk_a, ksk_b, lwe_a, lwe_b, out_a,
                                       out_b, batch, s),
             "key switch kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_bootstrap_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
+                        const uint64_t *lwe_a, const uint64_t *lwe_b, uint64_t lwe_q, const uint64_t *bsk_ntt,
+                        const uint64_t *test_poly, uint32_t ks_base_log, uint32_t ks_level, uint32_t out_dim,
+                        const uint64_t *ksk_a, const uint64_t *ksk_b, uint64_t *out_a, uint64_t *out_b, size_t batch,
+                        int where) {
+    FHE_MULTI(batch, where, lwe_b, fhe_bootstrap_batch(c, k, base_log, level, lwe_dim, lwe_a + lo * lwe_dim, lwe_b + lo,
+                                                       lwe_q, bsk_ntt, test_poly, ks_base_log, ks_level, out_dim,
+                                                       ksk_a, ksk_b, out_a + lo * out_dim, out_b + lo, nb, where));
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_tfhe(c, k, base_log, level));
+    if (lwe_q == 0) return fail(FHE_ERR_ZERO_MODULUS, "LWE modulus must be non-zero");
+    if (ks_base_log == 0 || ks_base_log > 63 || (ks_level > 0 && (u64)(ks_level - 1) * ks_base_log >= 64))
+        return fail(FHE_ERR_INVALID_ARG, "invalid key-switch decomposition (base_log, level)");
+    if (batch == 0) return FHE_OK;
+    const size_t n = c->n, in_dim = (size_t)k * n, entries = in_dim * ks_level;
+    if (!lwe_b || !test_poly || !out_b || (lwe_dim && (!lwe_a || !bsk_ntt)) || (entries && !ksk_b) ||
+        (entries && out_dim && !ksk_a) || (out_dim && !out_a))
+        return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t ggsw_words = (size_t)(k + 1) * level * (k + 1) * n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, lwe_a, batch * lwe_dim * 8, 1));
+    FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
+    FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
+    FHE_TRY(hs.map(where, test_poly, n * 8, 1));
+    FHE_TRY(hs.map(where, ksk_a, entries * out_dim * 8, 1));
+    FHE_TRY(hs.map(where, ksk_b, entries * 8, 1));
+    FHE_TRY(hs.map(where, out_a, batch * out_dim * 8, 2));
+    FHE_TRY(hs.map(where, out_b, batch * 8, 2));
+    int rc = FHE_OK;
+    {
+        // bootstrap_with_test_poly (bootstrap_engine.cpp:684-708): acc =
+        // (0, .., 0, test_poly) -> blind_rotate -> sample_extract ->
+        // key_switch (GLWE modulus), all on the context stream
+        StreamTemp tmp(c->stream);
+        u64 *acc = nullptr, *ea = nullptr, *eb = nullptr;
+        FHE_TRY(tmp.alloc(batch * (k + 1) * n * 8, acc));
+        FHE_TRY(tmp.alloc(batch * in_dim * 8, ea));
+        FHE_TRY(tmp.alloc(batch * 8, eb));
+        HIP_TRY(FHE_NS::launch_glwe_init(test_poly, acc, (uint32_t)n, k + 1, batch, c->stream), "glwe init kernel");
+        rc = fhe_blind_rotate_batch(c, k, base_log, level, lwe_dim, lwe_a, lwe_b, lwe_q, bsk_ntt, acc, batch,
+                                    FHE_DEVICE);
+        if (rc == FHE_OK) {
+            hipError_t e = FHE_NS::launch_sample_extract(mod_consts(c->q), acc, ea, eb, (uint32_t)n, k, batch, c->stream);
+            if (e == hipSuccess)
+                e = FHE_NS::launch_key_switch(mod_consts(c->q), ks_base_log, ks_level, (uint32_t)in_dim, out_dim, ksk_a,
+                                              ksk_b, ea, eb, out_a, out_b, batch, c->stream);
+            if (e != hipSuccess) rc = hip_fail(e, "bootstrap");
+        }
+    }
+    if (rc != FHE_OK) return rc;
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 

@@ -55,6 +55,21 @@ hipError_t launch_cmux(const Plan &p, int k1, int level, int base_log, const uin
 // Ciphertext multiply (coefficient form): x, y [batch][2][n] -> out [batch][3][n]
 hipError_t launch_ct_mul(const Plan &p, const uint64_t *x, const uint64_t *y, uint64_t *out, size_t batch);
 
+// EncryptionEngine encrypt / decrypt / add_plain (ntt_engine.hip); keys
+// prepared NTT x R (Montgomery form): pk_prep (pk.a, pk.b), sk_prep (s, s^2).
+// t = plaintext modulus (0 -> 4).  decrypt: phase [batch][n] is required for
+// comps == 3 on coefficient-form ciphertexts (the partial phase lives there);
+// store_phase selects whether the final phase is written.
+hipError_t launch_encrypt(const Plan &p, uint64_t t, const uint64_t *pk_prep, const uint64_t *vals,
+                          const uint64_t *u, const uint64_t *e1, const uint64_t *e2, uint64_t *ct, size_t batch);
+hipError_t launch_decrypt(const Plan &p, uint64_t t, const uint64_t *sk_prep, const uint64_t *ct, int comps,
+                          int is_ntt, uint64_t *phase, int store_phase, uint64_t *dec, uint64_t *noise, size_t batch);
+hipError_t launch_add_plain(const Plan &p, uint64_t t, const uint64_t *ct, const uint64_t *vals, int is_ntt,
+                            uint64_t *out, size_t batch);
+// acc [batch][k1][n] = (0, .., 0, test_poly): bootstrap's accumulator
+hipError_t launch_glwe_init(const uint64_t *test_poly, uint64_t *acc, uint32_t n, uint32_t k1, size_t batch,
+                            hipStream_t s);
+
 // Elementwise kernels (elementwise.hip).
 struct ModConsts {
     uint64_t q, mu, qinv, r2;  // mu = floor(2^64/q); Montgomery R = 2^64

@@ -449,7 +449,8 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
 struct NoFin {
     __device__ uint64_t operator()(uint32_t, uint64_t x) const { return x; }
 };
-template <int LOGN, bool NEGA, int PF = kPfSingle, typename W, typename F = NoFin>
+// STORE = false: fin() does every store itself (dst unused).
+template <int LOGN, bool NEGA, int PF = kPfSingle, bool STORE = true, typename W, typename F = NoFin>
 __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, uint64_t *__restrict__ dst,
                                                    bool valid, const NttArgs<W> &A, Tw<W> scale,
                                                    const Tw<W> *__restrict__ post, uint32_t sh = 0, uint32_t off = 0,
@@ -468,7 +469,8 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
         W x = v[t];
         if constexpr (NEGA) x = A.ar.shoup(x, post[gi | off]);
         const uint64_t y = fin(gi, (uint64_t)A.ar.red1q(x));
-        if constexpr (G::P == 1)
+        if constexpr (!STORE) (void)y;
+        else if constexpr (G::P == 1)
             bstore(brsrc(dst), (tau << sh) * 8u, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u, y);
         else if (valid)
             __builtin_nontemporal_store(y, dst + gi);

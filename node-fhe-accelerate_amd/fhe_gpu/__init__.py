@@ -138,6 +138,15 @@ SIGNATURES = [
     ("fhe_key_switch_batch", C.c_int,
      [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp, C.c_size_t, C.c_int,
       C.c_int, vp]),
+    ("fhe_secret_key_prepare", C.c_int, [vp, vp, vp, C.c_int]),
+    ("fhe_public_key_prepare", C.c_int, [vp, vp, vp, C.c_int]),
+    ("fhe_encrypt_batch", C.c_int, [vp, C.c_uint64, vp, vp, vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_decrypt_batch", C.c_int,
+     [vp, C.c_uint64, vp, vp, C.c_uint32, C.c_int, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_add_plain_batch", C.c_int, [vp, C.c_uint64, vp, vp, C.c_int, vp, C.c_size_t, C.c_int]),
+    ("fhe_bootstrap_batch", C.c_int,
+     [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint64, vp, vp, C.c_uint32, C.c_uint32,
+      C.c_uint32, vp, vp, vp, vp, C.c_size_t, C.c_int]),
     ("fhe_modmul_batch", C.c_int, [C.c_uint64, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
     ("fhe_ml_constants", C.c_int, [u64p, u64p]),
     ("fhe_ml_montmul_batch", C.c_int, [u64p, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
@@ -606,12 +615,152 @@ class EvaluationKey:
             _check(lib().fhe_relin_key_prepare(ring._h, self.level, bi.ptr, bo.ptr, w))
 
 
+class SecretKey:
+    """SecretKey (key_manager.h): the polynomial s [n] and its NTT-domain
+    form prepared once on the GPU (fhe_secret_key_prepare: s and s^2)."""
+
+    def __init__(self, ring: "PolynomialRing", poly):
+        s = _as_u64(poly)
+        if tuple(s.shape) != (ring.degree,):
+            raise FHEError(-9, "secret key must have shape [n]")
+        self.poly, self.ring = s, ring
+        self.prep = _empty(s, (2, ring.degree))
+        bi, bo = _Buf(s), _Buf(self.prep, True)
+        w = _where(bi, bo)
+        ring._bind_stream(w)
+        _check(lib().fhe_secret_key_prepare(ring._h, bi.ptr, bo.ptr, w))
+
+
+class PublicKey:
+    """PublicKey (key_manager.h:70-76): (a, b = a s + e) as [2, n], prepared
+    once into the NTT domain (fhe_public_key_prepare)."""
+
+    def __init__(self, ring: "PolynomialRing", a, b=None):
+        pk = _as_u64(a) if b is None else (torch.stack([_as_u64(a), _as_u64(b)]) if _is_tensor(a)
+                                            else np.stack([_as_u64(a), _as_u64(b)]))
+        if tuple(pk.shape) != (2, ring.degree):
+            raise FHEError(-9, "public key must have shape [2, n] = (a, b)")
+        self.poly, self.ring = pk, ring
+        self.prep = _like(pk)
+        bi, bo = _Buf(pk), _Buf(self.prep, True)
+        w = _where(bi, bo)
+        ring._bind_stream(w)
+        _check(lib().fhe_public_key_prepare(ring._h, bi.ptr, bo.ptr, w))
+
+
+class DecryptionResult:
+    """Batched DecryptionResult (encryption.h): decoded slot values
+    [..., n] (slot 0 is decrypt_value's result), the reference's noise budget
+    log2(q / (2 max_noise)) per ciphertext, and success = budget >= 0
+    (encryption.cpp:289-295)."""
+
+    def __init__(self, values, max_noise, modulus, phase=None):
+        import math
+
+        self.values, self.phase = values, phase
+        mx = np.asarray(max_noise.cpu() if _is_tensor(max_noise) else max_noise, dtype=np.uint64)
+        self.max_noise = mx
+        flat = mx.reshape(-1)
+        self.noise_budget = np.array([math.log2(float(modulus) / (2.0 * max(float(int(v)), 1.0))) for v in flat])
+        self.noise_budget = self.noise_budget.reshape(mx.shape)
+        self.success = self.noise_budget >= 0
+        self.error = ["" if ok else "Noise budget exhausted - decryption may be incorrect" for ok in
+                      self.success.reshape(-1)]
+
+
 class EncryptionEngine:
     """Ciphertext arithmetic of EncryptionEngine (encryption.cpp:594-980) over
-    batches of ciphertexts [..., 2, n] (c0, c1) / [..., 3, n] (degree 2)."""
+    batches of ciphertexts [..., 2, n] (c0, c1) / [..., 3, n] (degree 2), and
+    encrypt / decrypt / add_plain (:171-348, :638-665) with plaintext modulus
+    t (0 selects the reference's default 4, :40-46)."""
 
-    def __init__(self, ring: "PolynomialRing"):
+    def __init__(self, ring: "PolynomialRing", plaintext_modulus: int = 0):
         self.ring = ring
+        self.t = int(plaintext_modulus)
+        self.delta = ring.modulus // (self.t or 4)
+
+    def _slots(self, values, nb):
+        """Plaintext slot values -> [nb, n] (a scalar or a short vector is
+        zero-padded: encode_plaintext / encode_packed, :107-131)."""
+        n = self.ring.degree
+        if _is_tensor(values):
+            v = values.reshape(-1, values.shape[-1]) if values.dim() else values.reshape(1, 1)
+            if v.shape[-1] != n:
+                pad = torch.zeros((v.shape[0], n), dtype=v.dtype, device=v.device)
+                pad[:, : min(n, v.shape[-1])] = v[:, :n]
+                v = pad
+            if v.shape[0] == 1 and nb > 1:
+                v = v.expand(nb, n)
+            return v.contiguous()
+        v = np.asarray(values, dtype=np.uint64)
+        v = v.reshape(1, 1) if v.ndim == 0 else v.reshape(-1, v.shape[-1])
+        if v.shape[-1] != n:
+            pad = np.zeros((v.shape[0], n), dtype=np.uint64)
+            pad[:, : min(n, v.shape[-1])] = v[:, :n]
+            v = pad
+        if v.shape[0] == 1 and nb > 1:
+            v = np.broadcast_to(v, (nb, n))
+        return np.ascontiguousarray(v)
+
+    def encrypt(self, values, pk: PublicKey, u, e1, e2, out=None):
+        """encrypt_internal (:171-205) with the sampled polynomials supplied:
+        u (ternary), e1, e2 (error) [..., n]; values: plaintext slots
+        [..., n] (or fewer, zero-padded).  -> ct [..., 2, n]."""
+        r = self.ring
+        u, e1, e2 = _as_u64(u), _as_u64(e1), _as_u64(e2)
+        nb = r._batch(u)
+        vals = self._slots(values, nb)
+        if out is None:
+            out = _empty(u, tuple(u.shape[:-1]) + (2, r.degree))
+        bk, bv, bu, b1, b2, bo = _Buf(pk.prep), _Buf(vals), _Buf(u), _Buf(e1), _Buf(e2), _Buf(out, True)
+        if not (bv.count == bu.count == b1.count == b2.count == nb * r.degree):
+            raise FHEError(-9, "values, u, e1, e2 must all be [batch, n]")
+        w = _where(bk, bv, bu, b1, b2, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_encrypt_batch(r._h, self.t, bk.ptr, bv.ptr, bu.ptr, b1.ptr, b2.ptr, bo.ptr, nb, w))
+        return out
+
+    def decrypt(self, ct, sk: SecretKey, is_ntt: bool = False, with_phase: bool = False):
+        """decrypt / decrypt_packed (:234-348) for [..., 2, n] or degree-2
+        [..., 3, n] ciphertexts -> DecryptionResult."""
+        r = self.ring
+        ct = _as_u64(ct)
+        comps = int(ct.shape[-2]) if len(ct.shape) >= 2 else 0
+        if comps not in (2, 3):
+            raise FHEError(-9, "ciphertexts must be [..., 2, n] or [..., 3, n]")
+        nb = _lead(ct, (comps, r.degree))
+        lead = tuple(ct.shape[:-2])
+        vals = _empty(ct, lead + (r.degree,))
+        mx = _empty(ct, lead if lead else (1,))
+        ph = _empty(ct, lead + (r.degree,)) if with_phase else None
+        bs, bc, bv, bm = _Buf(sk.prep), _Buf(ct), _Buf(vals, True), _Buf(mx, True)
+        bp = _Buf(ph, True) if ph is not None else None
+        w = _where(bs, bc, bv, bm, bp)
+        r._bind_stream(w)
+        _check(lib().fhe_decrypt_batch(r._h, self.t, bs.ptr, bc.ptr, comps, int(bool(is_ntt)), bv.ptr,
+                                       bp.ptr if bp else None, bm.ptr, nb, w))
+        if _is_tensor(mx):
+            torch.cuda.current_stream(mx.device).synchronize()
+        return DecryptionResult(vals, mx, r.modulus, ph)
+
+    def decrypt_value(self, ct, sk: SecretKey, is_ntt: bool = False):
+        """decrypt_value (:303-310): slot 0, or None where decryption failed."""
+        res = self.decrypt(ct, sk, is_ntt)
+        v = res.values.cpu().numpy().view(np.uint64) if _is_tensor(res.values) else res.values
+        return [int(x) if ok else None for x, ok in zip(v.reshape(-1, self.ring.degree)[:, 0], res.success.reshape(-1))]
+
+    def add_plain(self, ct, values, is_ntt: bool = False, out=None):
+        """add_plain (:638-665): (c0 + encode(values), c1)."""
+        r = self.ring
+        ct = _as_u64(ct)
+        nb = _lead(ct, (2, r.degree))
+        vals = self._slots(values, nb)
+        out = _like(ct) if out is None else out
+        bc, bv, bo = _Buf(ct), _Buf(vals), _Buf(out, True)
+        w = _where(bc, bv, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_add_plain_batch(r._h, self.t, bc.ptr, bv.ptr, int(bool(is_ntt)), bo.ptr, nb, w))
+        return out
 
     def _pair(self, ct1, ct2):
         ct1, ct2 = _as_u64(ct1), _as_u64(ct2)
@@ -791,6 +940,44 @@ class BootstrapEngine:
         _check(lib().fhe_blind_rotate_batch(r._h, self.k, self.base_log, self.level, dim, bla.ptr, blb.ptr,
                                             lwe_q if lwe_q is not None else r.modulus, bk.ptr, ba.ptr, nb, w))
         return acc
+
+    def bootstrap(self, lwe_a, lwe_b, bsk_ntt, test_poly, ksk_a, ksk_b, ks_base_log: int, ks_level: int,
+                  lwe_q: Optional[int] = None):
+        """bootstrap_with_test_poly (bootstrap_engine.cpp:684-708) for a batch
+        of LWE ciphertexts (lwe_a [..., dim], lwe_b [...]): blind rotation of
+        (0, test_poly), sample extract, key switch (ksk_a [k*n*ks_level,
+        out_dim], ksk_b [k*n*ks_level]).  -> (a [..., out_dim], b [...])."""
+        r = self.ring
+        lwe_a, lwe_b, test_poly, ksk_a, ksk_b = (_as_u64(x) for x in (lwe_a, lwe_b, test_poly, ksk_a, ksk_b))
+        dim = int(lwe_a.shape[-1])
+        nb = _lead(lwe_a, (dim,))
+        out_dim = int(ksk_a.shape[-1])
+        out_a = _empty(lwe_a, tuple(lwe_a.shape[:-1]) + (out_dim,))
+        out_b = _like(lwe_b)
+        bla, blb, bk, bt, bka, bkb, boa, bob = (_Buf(lwe_a), _Buf(lwe_b), _Buf(bsk_ntt), _Buf(test_poly), _Buf(ksk_a),
+                                                _Buf(ksk_b), _Buf(out_a, True), _Buf(out_b, True))
+        if blb.count != nb or bt.count != r.degree or bkb.count != self.k * r.degree * ks_level or \
+                bka.count != bkb.count * out_dim:
+            raise FHEError(-9, "LWE / test polynomial / key-switching key shapes disagree")
+        w = _where(bla, blb, bk, bt, bka, bkb, boa, bob)
+        r._bind_stream(w)
+        _check(lib().fhe_bootstrap_batch(r._h, self.k, self.base_log, self.level, dim, bla.ptr, blb.ptr,
+                                         lwe_q if lwe_q is not None else r.modulus, bk.ptr, bt.ptr, ks_base_log,
+                                         ks_level, out_dim, bka.ptr, bkb.ptr, boa.ptr, bob.ptr, nb, w))
+        return out_a, out_b
+
+    programmable_bootstrap = bootstrap  # :716-722: the lookup table's polynomial as test_poly
+
+    def create_lookup_table(self, func, input_modulus: int, output_modulus: int):
+        """create_lookup_table (bootstrap_engine.cpp:725-758): the test
+        polynomial encoding func (host-side, O(n))."""
+        n, q = self.ring.degree, self.ring.modulus
+        delta_out = q // output_modulus
+        coeffs = np.zeros(n, dtype=np.uint64)
+        for i in range(n):
+            v = ((i * input_modulus + n) // (2 * n)) % input_modulus
+            coeffs[i] = ((int(func(v)) % output_modulus) * delta_out) % q
+        return coeffs
 
     def sample_extract(self, glwe):
         """sample_extract (:594-624) -> (a [..., k*n], b [...])."""

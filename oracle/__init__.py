@@ -87,6 +87,13 @@ def lib():
                                         u64p, C.c_uint64, u64p, u64p]
         L.oracle_ct_multiply.argtypes = [C.c_void_p, u64p, u64p, C.c_int, u64p]
         L.oracle_relinearize.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, u64p, u64p, u64p]
+        L.oracle_encode.argtypes = [C.c_uint64, C.c_uint64, u64p, C.c_uint32, u64p]
+        L.oracle_encrypt.argtypes = [C.c_void_p, C.c_uint64, u64p, u64p, u64p, u64p, u64p, u64p]
+        L.oracle_decrypt.argtypes = [C.c_void_p, C.c_uint64, u64p, u64p, C.c_uint32, C.c_int, u64p, u64p, u64p]
+        L.oracle_add_plain.argtypes = [C.c_void_p, C.c_uint64, u64p, u64p, C.c_int, u64p]
+        L.oracle_bootstrap.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u64p, C.c_uint64,
+                                       C.c_uint64, u64p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, u64p, u64p, u64p,
+                                       u64p]
         L.oracle_testrandom_coeffs.argtypes = [C.c_uint64, C.c_uint64, u64p, C.c_size_t]
         L.oracle_mt19937_64_raw.argtypes = [C.c_uint64, u64p, C.c_size_t]
         L.oracle_splitmix_fill.argtypes = [C.c_uint64, C.c_uint64, u64p, C.c_size_t, C.c_size_t]
@@ -264,6 +271,14 @@ def key_switch(q, base_log, level, ksk_a, ksk_b, lwe_a, lwe_b):
     return out_a, b.value
 
 
+def encode(q, t, values):
+    """encode_packed (encryption.cpp:117-131)."""
+    values = np.ascontiguousarray(values, dtype=np.uint64)
+    out = np.empty_like(values)
+    lib().oracle_encode(q, t, _p(values), values.size, _p(out))
+    return out
+
+
 def testrandom_coeffs(seed, q, count):
     out = np.empty(count, dtype=np.uint64)
     lib().oracle_testrandom_coeffs(seed, q, _p(out), count)
@@ -372,6 +387,41 @@ class NTT:
         out = np.empty((2, self.n), dtype=np.uint64)
         lib().oracle_relinearize(self._h, base_log, level, _p(ct3), _p(rlk), _p(out))
         return out
+
+    # ---- EncryptionEngine encrypt / decrypt / add_plain, BootstrapEngine::bootstrap
+    def encrypt(self, t, pk, values, u, e1, e2):
+        """encrypt_internal (encryption.cpp:171-205); pk [2, n] = (a, b)."""
+        pk, values, u, e1, e2 = (np.ascontiguousarray(x, dtype=np.uint64) for x in (pk, values, u, e1, e2))
+        out = np.empty((2, self.n), dtype=np.uint64)
+        lib().oracle_encrypt(self._h, t, _p(pk), _p(values), _p(u), _p(e1), _p(e2), _p(out))
+        return out
+
+    def decrypt(self, t, sk, ct, is_ntt=False):
+        """decrypt (:234-300) -> (values [n], phase [n], max_noise)."""
+        sk, ct = (np.ascontiguousarray(x, dtype=np.uint64) for x in (sk, ct))
+        comps = ct.shape[0]
+        vals = np.empty(self.n, dtype=np.uint64)
+        ph = np.empty(self.n, dtype=np.uint64)
+        mx = np.zeros(1, dtype=np.uint64)
+        lib().oracle_decrypt(self._h, t, _p(sk), _p(ct), comps, int(is_ntt), _p(vals), _p(ph), _p(mx))
+        return vals, ph, int(mx[0])
+
+    def add_plain(self, t, ct, values, is_ntt=False):
+        ct, values = (np.ascontiguousarray(x, dtype=np.uint64) for x in (ct, values))
+        out = np.empty((2, self.n), dtype=np.uint64)
+        lib().oracle_add_plain(self._h, t, _p(ct), _p(values), int(is_ntt), _p(out))
+        return out
+
+    def bootstrap(self, k, base_log, level, lwe_a, lwe_b, lwe_q, bsk, test_poly, ks_base_log, ks_level, ksk_a, ksk_b):
+        """bootstrap_with_test_poly (bootstrap_engine.cpp:684-708) -> (a [out_dim], b)."""
+        lwe_a, bsk, test_poly, ksk_a, ksk_b = (np.ascontiguousarray(x, dtype=np.uint64)
+                                               for x in (lwe_a, bsk, test_poly, ksk_a, ksk_b))
+        out_dim = ksk_a.shape[-1]
+        oa = np.empty(out_dim, dtype=np.uint64)
+        ob = np.zeros(1, dtype=np.uint64)
+        lib().oracle_bootstrap(self._h, k, base_log, level, lwe_a.size, _p(lwe_a), int(lwe_b), lwe_q, _p(bsk),
+                               _p(test_poly), ks_base_log, ks_level, out_dim, _p(ksk_a), _p(ksk_b), _p(oa), _p(ob))
+        return oa, int(ob[0])
 
     def batch_threaded(self, op, a, b=None, c=None, threads=1):
         """op: 0 fwd (in place), 1 inv (in place), 2 polymul, 3 fwd+mul."""

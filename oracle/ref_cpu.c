@@ -662,6 +662,110 @@ void oracle_relinearize(const oracle_ntt *t, u32 base_log, u32 level, const u64 
 }
 
 /* ------------------------------------------------------------------------
+ * EncryptionEngine encrypt / decrypt / add_plain (encryption.cpp) with the
+ * sampled polynomials (u, e1, e2) supplied by the caller, so the function
+ * is deterministic.
+ * ------------------------------------------------------------------------ */
+/* delta_ = q / t, t = plaintext_modulus or 4 when 0 (encryption.cpp:40-46) */
+static u64 ee_t(u64 t) { return t ? t : 4; }
+/* encode_packed (:117-131): coeffs[i] = (values[i] * delta) % q, u64 product
+ * (wraps); encode_plaintext (:107-115) is the one-value case. */
+void oracle_encode(u64 q, u64 t, const u64 *values, u32 n, u64 *out) {
+    const u64 delta = q / ee_t(t);
+    for (u32 i = 0; i < n; ++i) out[i] = (values[i] * delta) % q;
+}
+/* encrypt_internal (:171-205): c0 = from_ntt(to_ntt(pk.b) . to_ntt(u)) + e1
+ * + m, c1 = from_ntt(to_ntt(pk.a) . to_ntt(u)) + e2 (add_inplace: mod_add).
+ * pk [2][n] = (a, b) (PublicKey field order, key_manager.h:70-76);
+ * ct out [2][n]. */
+void oracle_encrypt(const oracle_ntt *t, u64 pt_mod, const u64 *pk, const u64 *values, const u64 *u,
+                    const u64 *e1, const u64 *e2, u64 *ct) {
+    const u32 n = t->n; const u64 q = t->q;
+    u64 *w = (u64 *)malloc(sizeof(u64) * n * 4);
+    u64 *un = w, *pb = w + n, *pa = w + 2 * n, *m = w + 3 * n;
+    memcpy(un, u, 8 * (size_t)n); memcpy(pa, pk, 8 * (size_t)n); memcpy(pb, pk + n, 8 * (size_t)n);
+    oracle_ntt_forward(t, un); oracle_ntt_forward(t, pa); oracle_ntt_forward(t, pb);
+    oracle_encode(q, pt_mod, values, n, m);
+    oracle_pointwise(q, pb, un, ct, n);
+    oracle_ntt_inverse(t, ct);
+    oracle_poly_add(q, ct, e1, ct, n);
+    oracle_poly_add(q, ct, m, ct, n);
+    oracle_pointwise(q, pa, un, ct + n, n);
+    oracle_ntt_inverse(t, ct + n);
+    oracle_poly_add(q, ct + n, e2, ct + n, n);
+    free(w);
+}
+/* decrypt (:234-300) + decode_packed (:150-163) + compute_noise_budget
+ * (:364-400).  ct [comps][n] (comps 2 or 3); is_ntt as Ciphertext::is_ntt.
+ * phase [n] = c0 - c1 s (- c2 s^2); values [n] = round(phase * t / q) % t;
+ * *max_noise = max_i |phase_i - round_i * delta| (wrapped at q/2), the
+ * integer whose double the reference's budget log2(q / (2 max)) uses. */
+void oracle_decrypt(const oracle_ntt *t, u64 pt_mod, const u64 *sk, const u64 *ct, u32 comps, int is_ntt,
+                    u64 *values, u64 *phase, u64 *max_noise) {
+    const u32 n = t->n; const u64 q = t->q, tt = ee_t(pt_mod), delta = q / tt;
+    u64 *w = (u64 *)malloc(sizeof(u64) * n * 5);
+    u64 *c1 = w, *s = w + n, *c1s = w + 2 * n, *c0 = w + 3 * n, *tmp = w + 4 * n;
+    memcpy(c1, ct + n, 8 * (size_t)n);
+    if (!is_ntt) oracle_ntt_forward(t, c1);
+    memcpy(s, sk, 8 * (size_t)n);
+    oracle_ntt_forward(t, s);
+    oracle_pointwise(q, c1, s, c1s, n);
+    oracle_ntt_inverse(t, c1s);
+    memcpy(c0, ct, 8 * (size_t)n);
+    if (is_ntt) oracle_ntt_inverse(t, c0);
+    oracle_poly_sub(q, c0, c1s, phase, n);
+    if (comps == 3) {
+        u64 *s2 = c1, *c2 = c0;  /* reuse */
+        oracle_pointwise(q, s, s, s2, n);
+        memcpy(c2, ct + 2 * (size_t)n, 8 * (size_t)n);
+        if (!is_ntt) oracle_ntt_forward(t, c2);
+        oracle_pointwise(q, c2, s2, tmp, n);
+        oracle_ntt_inverse(t, tmp);
+        oracle_poly_sub(q, phase, tmp, phase, n);
+    }
+    u64 mx = 0;
+    for (u32 i = 0; i < n; ++i) {
+        const u64 c = phase[i];
+        const u64 rounded = (u64)(((u128)c * tt + q / 2) / q);
+        values[i] = rounded % tt;
+        const u64 expected = (rounded * delta) % q;
+        int64_t noise = c >= expected ? (int64_t)(c - expected) : (int64_t)(expected - c);
+        if (noise > (int64_t)(q / 2)) noise = (int64_t)q - noise;
+        const u64 a = (u64)(noise < 0 ? -noise : noise);
+        if (a > mx) mx = a;
+    }
+    *max_noise = mx;
+    free(w);
+}
+/* add_plain (:638-665): c0 + encode(values) (to_ntt'd first when the
+ * ciphertext is in the NTT domain), c1 copied.  ct, out [2][n]. */
+void oracle_add_plain(const oracle_ntt *t, u64 pt_mod, const u64 *ct, const u64 *values, int is_ntt, u64 *out) {
+    const u32 n = t->n;
+    u64 *m = (u64 *)malloc(sizeof(u64) * n);
+    oracle_encode(t->q, pt_mod, values, n, m);
+    if (is_ntt) oracle_ntt_forward(t, m);
+    oracle_poly_add(t->q, ct, m, out, n);
+    memcpy(out + n, ct + n, 8 * (size_t)n);
+    free(m);
+}
+/* BootstrapEngine::bootstrap_with_test_poly (bootstrap_engine.cpp:684-708):
+ * acc = (0, .., 0, test_poly); blind_rotate; sample_extract; key_switch
+ * with the GLWE modulus.  Out: out_a [out_dim], *out_b. */
+void oracle_bootstrap(const oracle_ntt *t, u32 k, u32 base_log, u32 level, u32 lwe_dim, const u64 *lwe_a,
+                      u64 lwe_b, u64 lwe_q, const u64 *bsk, const u64 *test_poly, u32 ks_base_log,
+                      u32 ks_level, u32 out_dim, const u64 *ksk_a, const u64 *ksk_b, u64 *out_a, u64 *out_b) {
+    const u32 n = t->n;
+    u64 *acc = (u64 *)calloc((size_t)(k + 1) * n, sizeof(u64));
+    u64 *ea = (u64 *)malloc(sizeof(u64) * ((size_t)k * n + 1));
+    u64 eb = 0;
+    memcpy(acc + (size_t)k * n, test_poly, 8 * (size_t)n);
+    oracle_blind_rotate(t, k, base_log, level, lwe_dim, lwe_a, lwe_b, lwe_q, bsk, acc);
+    oracle_sample_extract(t->q, k, n, acc, ea, &eb);
+    oracle_key_switch(t->q, ks_base_log, ks_level, k * n, out_dim, ksk_a, ksk_b, ea, eb, out_a, out_b);
+    free(acc); free(ea);
+}
+
+/* ------------------------------------------------------------------------
  * Test-input generators
  * ------------------------------------------------------------------------ */
 /* std::mt19937_64 (used by TestRandom, cpp/tests/test_harness.h:29-73);

@@ -234,3 +234,98 @@ def test_cipher_golden(golden_dir):
             acc = np.array(c["acc"], np.uint64).reshape(2, n)
             got = t.blind_rotate(1, c["base_log"], lv, np.array(c["lwe_a"], np.uint64), c["lwe_b"], q, bsk, acc)
             assert I(got) == c["out"]
+
+
+# ---- EncryptionEngine encrypt / decrypt / add_plain, BootstrapEngine::bootstrap
+def py_encode(q, t, values):  # encryption.cpp:107-131 (u64 product wraps)
+    delta = q // (t or 4)
+    return [((v * delta) & M64) % q for v in I(values)]
+
+
+def py_encrypt(q, t, pk, values, u, e1, e2):  # :171-205
+    un = pyref.forward(I(u), q)
+    c0 = pyref.inverse(pw(q, pyref.forward(I(pk[1]), q), un), q)  # pk = (a, b)
+    c0 = [mod_add(q, a, b) for a, b in zip(c0, I(e1))]
+    c0 = [mod_add(q, a, b) for a, b in zip(c0, py_encode(q, t, values))]
+    c1 = pyref.inverse(pw(q, pyref.forward(I(pk[0]), q), un), q)
+    c1 = [mod_add(q, a, b) for a, b in zip(c1, I(e2))]
+    return [c0, c1]
+
+
+def py_decrypt(q, t, sk, ct, is_ntt=False):  # :234-300, :150-163, :364-400
+    c1 = I(ct[1]) if is_ntt else pyref.forward(I(ct[1]), q)
+    s = pyref.forward(I(sk), q)
+    c0 = pyref.inverse(I(ct[0]), q) if is_ntt else I(ct[0])
+    res = [mod_sub(q, a, b) for a, b in zip(c0, pyref.inverse(pw(q, c1, s), q))]
+    if len(ct) == 3:
+        c2 = I(ct[2]) if is_ntt else pyref.forward(I(ct[2]), q)
+        res = [mod_sub(q, a, b) for a, b in zip(res, pyref.inverse(pw(q, c2, pw(q, s, s)), q))]
+    tt = t or 4
+    delta = q // tt
+    vals, mx = [], 0
+    for c in res:
+        rounded = (c * tt + q // 2) // q
+        vals.append(rounded % tt)
+        noise = abs(c - (rounded * delta) % q)
+        if noise > q // 2:
+            noise = q - noise
+        mx = max(mx, noise)
+    return vals, res, mx
+
+
+def py_add_plain(q, t, ct, values, is_ntt=False):  # :638-665
+    m = py_encode(q, t, values)
+    if is_ntt:
+        m = pyref.forward(m, q)
+    return [[mod_add(q, a, b) for a, b in zip(I(ct[0]), m)], I(ct[1])]
+
+
+@pytest.mark.parametrize("n,q,t", [(16, 97, 4), (64, 7681, 16), (32, P62, 0), (128, P27, 1 << 40)])
+def test_encrypt_decrypt_oracle_vs_python(n, q, t):
+    o = oracle.NTT(n, q)
+    pk, u, e1, e2, sk = rnd(21, q, 2, n), rnd(22, 3, n), rnd(23, q, n), rnd(24, q, n), rnd(25, 3, n)
+    vals = rnd(26, t or 4, n)
+    vals[0] = M64  # the u64 product wraps before % q
+    ct = o.encrypt(t, pk, vals, u, e1, e2)
+    assert [I(r) for r in ct] == py_encrypt(q, t, pk, vals, u, e1, e2)
+    ct3 = rnd(27, q, 3, n)
+    for c, is_ntt in ((ct, False), (ct, True), (ct3, False), (ct3, True)):
+        v, ph, mx = o.decrypt(t, sk, c, is_ntt)
+        ev, eph, emx = py_decrypt(q, t, sk, c, is_ntt)
+        assert I(v) == ev and I(ph) == eph and mx == emx
+    for is_ntt in (False, True):
+        assert [I(r) for r in o.add_plain(t, ct, vals, is_ntt)] == py_add_plain(q, t, ct, vals, is_ntt)
+
+
+@pytest.mark.parametrize("n,q,t", [(64, 7681, 16), (1024, P27, 4), (256, P62, 1 << 20)])
+def test_noise_free_encryption_decrypts(n, q, t):
+    """Algebraic pin of the restated encrypt/decrypt: the reference's product
+    inv(fwd(a) . fwd(b)) is the pointwise algebra carried back through one
+    linear bijection, hence commutative and associative.  With pk = (a, a*s)
+    and e1 = e2 = 0, decrypt(encrypt(m)) = c0 - c1 s = (a s) u + m delta -
+    (a u) s = m delta exactly: the values come back and the max noise is 0."""
+    o = oracle.NTT(n, q)
+    a, s, u = rnd(31, q, n), rnd(32, 3, n), rnd(33, 3, n)
+    m = rnd(34, t, n)
+    pk = np.stack([a, o.polymul(a, s)])
+    z = np.zeros(n, np.uint64)
+    ct = o.encrypt(t, pk, m, u, z, z)
+    v, ph, mx = o.decrypt(t, s, ct)
+    assert (v == m).all() and mx == 0
+    assert (ph == oracle.encode(q, t, m)).all()
+
+
+@pytest.mark.parametrize("n,q,bl,lv,dim", [(16, 97, 2, 3, 5), (32, 193, 3, 2, 4)])
+def test_bootstrap_oracle_vs_python(n, q, bl, lv, dim):
+    o = oracle.NTT(n, q)
+    bsk = rnd(41, q, dim, 2 * lv, 2, n)
+    lwe_a, test_poly = rnd(42, q, dim), rnd(43, q, n)
+    ks_bl, ks_lv, out_dim = 3, 2, 7
+    ksk_a, ksk_b = rnd(44, q, n * ks_lv, out_dim), rnd(45, q, n * ks_lv)
+    oa, ob = o.bootstrap(1, bl, lv, lwe_a, 29, q, bsk, test_poly, ks_bl, ks_lv, ksk_a, ksk_b)
+    acc = np.zeros((2, n), np.uint64)
+    acc[1] = test_poly
+    acc = np.array(py_blind_rotate(acc, lwe_a, 29, bsk, q, bl, lv), dtype=np.uint64)
+    ea = [int(acc[0][0])] + [(q - int(acc[0][n - j])) % q for j in range(1, n)]
+    ra, rb = py_key_switch(q, ks_bl, ks_lv, ksk_a, ksk_b, np.array(ea, np.uint64), int(acc[1][0]))
+    assert I(oa) == ra and ob == rb
