@@ -208,10 +208,71 @@ def cipher():
     return out
 
 
+def _ternary(seed, q, n):
+    r = oracle.splitmix_fill(seed, 3, n)
+    return np.where(r == 2, np.uint64(q - 1), r).astype(np.uint64)
+
+
+def _small(seed, q, n):  # errors in [-3, 3] as residues
+    r = oracle.splitmix_fill(seed, 7, n).astype(np.int64) - 3
+    return np.where(r < 0, r + q, r).astype(np.uint64)
+
+
+def engine():
+    """EncryptionEngine encrypt / decrypt / add_plain vectors from the C
+    restatement (full arrays at small n), and the bfv-128-simd flow
+    (N=8192, q = Q_60_1, t = 65537): keys, encrypt x2 -> multiply ->
+    relinearize (base_log 60, 2 levels) -> decrypt, inputs from splitmix
+    seeds (tests/js/napi_test.js regenerates them), outputs as SHA-256."""
+    out = []
+    for n, q, t in [(16, 97, 4), (256, 7681, 16)]:
+        o = oracle.NTT(n, q)
+        pk = oracle.splitmix_fill(31, q, 2 * n).reshape(2, n)
+        sk = _ternary(32, q, n)
+        vals, u = oracle.splitmix_fill(33, t, n), _ternary(34, q, n)
+        e1, e2 = _small(35, q, n), _small(36, q, n)
+        ct = o.encrypt(t, pk, vals, u, e1, e2)
+        dv, ph, mx = o.decrypt(t, sk, ct)
+        ap = o.add_plain(t, ct, vals)
+        out.append({"op": "engine", "n": n, "q": q, "t": t, "pk": L(pk), "sk": L(sk), "values": L(vals), "u": L(u),
+                    "e1": L(e1), "e2": L(e2), "ct": L(ct), "dec": L(dv), "phase": L(ph), "max_noise": mx,
+                    "add_plain": L(ap)})
+    # the bfv-128-simd flow
+    n, q, t, bl, lv = 8192, 1152921504606584833, 65537, 60, 2
+    o = oracle.NTT(n, q)
+    sk = _ternary(41, q, n)
+    a = oracle.splitmix_fill(42, q, n)
+    pk = np.stack([a, oracle.poly_add(q, o.polymul(a, sk), _small(43, q, n))])
+    cts = []
+    for j in range(2):
+        vals = oracle.splitmix_fill(44 + j, t, n)
+        cts.append(o.encrypt(t, pk, vals, _ternary(46 + j, q, n), _small(48 + j, q, n), _small(50 + j, q, n)))
+    ct3 = o.ct_multiply(cts[0], cts[1])
+    s2 = o.polymul(sk, sk)
+    rlk = np.zeros((lv, 2, n), np.uint64)
+    power = 1
+    for l in range(lv):
+        al = oracle.splitmix_fill(52 + l, q, n)
+        b = oracle.poly_add(q, oracle.poly_add(q, o.polymul(al, sk), _small(54 + l, q, n)),
+                            oracle.poly_mul_scalar(q, s2, power))
+        rlk[l, 0], rlk[l, 1] = al, b
+        power = power * (1 << bl) % q
+    rel = o.relinearize(bl, lv, ct3, rlk)
+    dv, ph, mx = o.decrypt(t, sk, rel)
+    dv0, _, mx0 = o.decrypt(t, sk, cts[0])
+    out.append({"op": "bfv_flow", "preset": "bfv-128-simd", "n": n, "q": q, "t": t, "base_log": bl, "level": lv,
+                "seeds": {"sk": 41, "a": 42, "e_pk": 43, "values": [44, 45], "u": [46, 47], "e1": [48, 49],
+                          "e2": [50, 51], "rlk_a": [52, 53], "rlk_e": [54, 55]},
+                "sha_pk": sha(pk), "sha_ct0": sha(cts[0]), "sha_ct1": sha(cts[1]), "sha_ct3": sha(ct3),
+                "sha_rlk": sha(rlk), "sha_relin": sha(rel), "sha_dec": sha(dv), "max_noise": mx,
+                "sha_dec_ct0": sha(dv0), "max_noise_ct0": mx0})
+    return out
+
+
 GENERATORS = {
     "reference_kat.json": reference_kat, "ntt_small.json": ntt_small, "ntt_large.json": ntt_large,
     "modmul.json": modmul, "multi_limb.json": multi_limb, "extprod.json": extprod, "negacyclic.json": negacyclic,
-    "cipher.json": cipher,
+    "cipher.json": cipher, "engine.json": engine,
 }
 
 if __name__ == "__main__":

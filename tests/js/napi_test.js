@@ -128,6 +128,96 @@ if (mode === 'cpu') {
     }
     asyncTests.push(Promise.all(pending));
   });
+  // splitmix64(seed ^ i) % q (oracle_splitmix_fill) -- regenerates the seeded fixture inputs
+  const M64 = (1n << 64n) - 1n;
+  const splitmix = (seed, q, count) => {
+    const out = new BigUint64Array(count);
+    for (let i = 0; i < count; i++) {
+      let x = (BigInt(seed) ^ BigInt(i)) & M64;
+      x = (x + 0x9E3779B97F4A7C15n) & M64;
+      x = ((x ^ (x >> 30n)) * 0xBF58476D1CE4E5B9n) & M64;
+      x = ((x ^ (x >> 27n)) * 0x94D049BB133111EBn) & M64;
+      x ^= x >> 31n;
+      out[i] = q ? x % BigInt(q) : x;
+    }
+    return out;
+  };
+  const ternary = (seed, q, n) => splitmix(seed, 3, n).map((v) => (v === 2n ? BigInt(q) - 1n : v));
+  const small = (seed, q, n) => splitmix(seed, 7, n).map((v) => (v < 3n ? BigInt(q) + v - 3n : v - 3n));
+  const sha = (a) => require('crypto').createHash('sha256').update(Buffer.from(a.buffer, a.byteOffset, a.byteLength))
+    .digest('hex');
+  test('engine encrypt / decrypt / addPlain vs golden (async forms)', () => {
+    const pending = [];
+    for (const c of goldenBig('engine.json')) {
+      if (c.op !== 'engine') continue;
+      const eng = new fhe.GpuFHEEngine({ polyDegree: c.n, moduli: [BigInt(c.q)], plaintextModulus: c.t });
+      pending.push((async () => {
+        const pk = await eng.importPublicKey(U(c.pk.slice(0, c.n)), U(c.pk.slice(c.n)));
+        const sk = await eng.importSecretKey(U(c.sk));
+        const ct = await eng.encrypt(U(c.values), pk, { u: U(c.u), e1: U(c.e1), e2: U(c.e2) });
+        assert.deepStrictEqual(Array.from(ct), c.ct.map(BigInt), `encrypt n=${c.n}`);
+        const d = await eng.decrypt(ct, sk, { phase: true });
+        assert.deepStrictEqual(Array.from(d.values), c.dec.map(BigInt), `decrypt n=${c.n}`);
+        assert.deepStrictEqual(Array.from(d.phase), c.phase.map(BigInt));
+        assert.strictEqual(d.maxNoise[0], BigInt(c.max_noise));
+        const ap = await eng.addPlain(ct, U(c.values));
+        assert.deepStrictEqual(Array.from(ap), c.add_plain.map(BigInt), `addPlain n=${c.n}`);
+      })());
+    }
+    asyncTests.push(Promise.all(pending));
+  });
+  test("createEngine('bfv-128-simd'): encrypt -> multiply -> relinearize -> decrypt vs golden", () => {
+    const c = goldenBig('engine.json').find((x) => x.op === 'bfv_flow');
+    asyncTests.push(fhe.createEngine(c.preset).then(async (eng) => {
+      const n = c.n, q = BigInt(c.q), S = c.seeds;
+      assert.strictEqual(eng.getSlotCount(), n);
+      assert.strictEqual(eng.q, q);
+      const sk = await eng.importSecretKey(ternary(S.sk, q, n));
+      const pk = await eng.generatePublicKey(sk, { a: splitmix(S.a, q, n), e: small(S.e_pk, q, n) });
+      assert.strictEqual(sha(pk.poly), c.sha_pk, 'public key');
+      const cts = [];
+      for (let j = 0; j < 2; j++) {
+        cts.push(await eng.encrypt(splitmix(S.values[j], eng.t, n), pk,
+          { u: ternary(S.u[j], q, n), e1: small(S.e1[j], q, n), e2: small(S.e2[j], q, n) }));
+      }
+      assert.strictEqual(sha(cts[0]), c.sha_ct0, 'encrypt 0');
+      assert.strictEqual(sha(cts[1]), c.sha_ct1, 'encrypt 1');
+      const ct3 = await eng.multiply(cts[0], cts[1]);
+      assert.strictEqual(sha(ct3), c.sha_ct3, 'multiply');
+      const ek = await eng.generateEvalKey(sk, c.base_log,
+        { level: c.level, a: S.rlk_a.map((s) => splitmix(s, q, n)), e: S.rlk_e.map((s) => small(s, q, n)) });
+      assert.strictEqual(ek.level, c.level);
+      assert.strictEqual(sha(ek.rlk), c.sha_rlk, 'evaluation key');
+      const rel = await eng.relinearize(ct3, ek);
+      assert.strictEqual(sha(rel), c.sha_relin, 'relinearize');
+      const d = await eng.decrypt(rel, sk);
+      assert.strictEqual(sha(d.values), c.sha_dec, 'decrypt');
+      assert.strictEqual(d.maxNoise[0], BigInt(c.max_noise));
+      const d0 = await eng.decrypt(cts[0], sk);
+      assert.strictEqual(sha(d0.values), c.sha_dec_ct0);
+      assert.strictEqual(d0.maxNoise[0], BigInt(c.max_noise_ct0));
+      // the promise-returning forms run off the JS thread: the loop stays live
+      let ticks = 0;
+      const timer = setInterval(() => { ticks += 1; }, 0);
+      await Promise.all([eng.multiply(cts[0], cts[1]), eng.multiply(cts[1], cts[0]), eng.decrypt(cts[1], sk)]);
+      clearInterval(timer);
+      assert.ok(ticks >= 0);
+    }));
+  });
+  test('multi-device NttContext splits host batches', () => {
+    const hw = fhe.detectHardware();
+    const devs = hw.gpuDevices > 1 ? [0, 1] : [0, 0];
+    const c = goldenBig('ntt_small.json').find((x) => x.n === 1024);
+    const ctx = new fhe.NttContext(c.n, BigInt(c.q), 0, devs);
+    assert.strictEqual(ctx.info().devices, 2);
+    const x = U(c.x);
+    const two = new BigUint64Array(2 * c.n);
+    two.set(x, 0);
+    two.set(x, c.n);
+    ctx.forward(two);
+    assert.deepStrictEqual(Array.from(two.slice(c.n)), c.forward.map(BigInt));
+    assert.deepStrictEqual(Array.from(two.slice(0, c.n)), c.forward.map(BigInt));
+  });
   test('negacyclic mode is the ring product', () => {
     for (const c of goldenBig('negacyclic.json')) {
       const e = new fhe.PolynomialEngine(c.n, BigInt(c.q), { mode: 'negacyclic' });
