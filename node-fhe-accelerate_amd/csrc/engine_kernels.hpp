@@ -98,7 +98,7 @@ k_encrypt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
     constexpr int STASH = eng_stash<LOGN, W>();
     __shared__ W lds_all[G::P * G::LW + (STASH == 1 ? G::P * G::N : 0)];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < E.batch;
     if (G::P == 1 && !valid) return;
@@ -162,7 +162,7 @@ k_decrypt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::LW];
     __shared__ unsigned long long nmax[G::P];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < E.batch;
     if (G::P == 1 && !valid) return;
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (eng_occ4<LOGN, W>()))
 k_add_plain_ntt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::LW];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < E.batch;
     if (G::P == 1 && !valid) return;

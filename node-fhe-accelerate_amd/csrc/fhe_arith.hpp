@@ -29,6 +29,12 @@ __device__ __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return a < b 
 // Twiddle with its Shoup companion w' = floor(w * 2^W / q).
 template <typename W> struct Tw { W w, wp; };
 
+// 32-bit forward (CT) twiddle tables hold -w mod 2^32 in Tw::w (Arith::ct).
+#ifndef FHE_NEG_FWD_TW
+#define FHE_NEG_FWD_TW 1
+#endif
+constexpr bool kNegFwdTw = FHE_NEG_FWD_TW;
+
 template <typename W>
 struct Arith {
     W q, q2;      // q, 2q
@@ -44,16 +50,26 @@ struct Arith {
 #ifndef FHE_SHOUP_ASM
 #define FHE_SHOUP_ASM 1
 #endif
+#ifndef FHE_MAD_EARLYCLOBBER
+#define FHE_MAD_EARLYCLOBBER 1
+#endif
         if constexpr (sizeof(W) == 4 && FHE_SHOUP_ASM) {
             // One v_mad_u64_u32 for x*w - h*q (mod 2^32): LLVM narrows the
             // 64-bit form below to two v_mul_lo_u32 + v_sub.  Only the low
             // half of the addend matters, so its high half is left undefined
             // (no zeroing move).
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            // Early-clobber destination: with dst overlapping the addend the
+            // hazard recognizer pads every such mad with an s_nop (measured:
+            // 1 per butterfly).
             u32x2 c;
             c.x = x * w;
             uint64_t r, cy;
+#if FHE_MAD_EARLYCLOBBER
+            asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=&s"(cy) : "v"(h), "s"(0u - q), "v"(c));
+#else
             asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "v"(h), "s"(0u - q), "v"(c));
+#endif
             (void)cy;
             return (W)r;
         } else if constexpr (sizeof(W) == 4 && FHE_SHOUP_MAD) {
@@ -77,19 +93,45 @@ struct Arith {
     __device__ __forceinline__ W red1q(W x) const { return umin(x, W(x - q)); }   // [0,2q)->[0,q)
     __device__ __forceinline__ W canon4(W x) const { return red1q(red2q(x)); }     // [0,4q)->[0,q)
 
+    // 32-bit forward twiddles are stored negated, {-w mod 2^32, w'}
+    // (kNegFwdTw): one v_mad_u64_u32 then yields nb = h*q - y*w = -b (mod
+    // 2^32), and the butterfly is x - nb, x + nb + 2q: a v_sub and a v_add3
+    // instead of an add, a sub and an add.
+    __device__ __forceinline__ W shoup_neg(W y, Tw<W> t) const {
+        const W h = mulhi(y, t.wp);
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 c;
+        c.x = y * t.w;  // y * (-w)
+        uint64_t r, cy;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=&s"(cy) : "v"(h), "s"(q), "v"(c));
+        (void)cy;
+        return (W)r;
+    }
     // Harvey forward (Cooley-Tukey) butterfly, values in [0, 4q).
     __device__ __forceinline__ void ct(W &x, W &y, Tw<W> t) const {
         W a = red2q(x);
-        W b = shoup(y, t);
-        x = a + b;
-        y = a - b + q2;
+        if constexpr (sizeof(W) == 4 && FHE_NEG_FWD_TW) {
+            const W nb = shoup_neg(y, t);
+            x = a - nb;
+            y = a + nb + q2;
+        } else {
+            W b = shoup(y, t);
+            x = a + b;
+            y = a - b + q2;
+        }
     }
     // Forward butterfly without reducing x: outputs grow by 2q per stage.
     __device__ __forceinline__ void ct_lazy(W &x, W &y, Tw<W> t) const {
-        W b = shoup(y, t);
         W a = x;
-        x = a + b;
-        y = a - b + q2;
+        if constexpr (sizeof(W) == 4 && FHE_NEG_FWD_TW) {
+            const W nb = shoup_neg(y, t);
+            x = a - nb;
+            y = a + nb + q2;
+        } else {
+            W b = shoup(y, t);
+            x = a + b;
+            y = a - b + q2;
+        }
     }
     // Stage-0 butterfly that also multiplies by R = 2^W (twiddle 1 -> R):
     // puts the transform in Montgomery form for a following pointwise

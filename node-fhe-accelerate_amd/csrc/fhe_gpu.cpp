@@ -174,6 +174,8 @@ int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
     }
     twf[0] = make_tw<W>(1, q);
     twi[0] = make_tw<W>(1, q);
+    if constexpr (sizeof(W) == 4 && FHE_NS::kNegFwdTw)
+        for (auto &t : twf) t.w = (W)(0u - t.w);  // Arith::ct's negated-twiddle butterfly
     const u64 R = (u64)((((u128)1) << BITS) % q);
     const u64 ninv_r = mulmod(c->inv_n, R, q);
     for (u32 i = 0; i < n; ++i) {

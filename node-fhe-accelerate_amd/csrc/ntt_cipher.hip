@@ -56,7 +56,7 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     using G = Geo<LOGN>;
     constexpr int NL = ctmul_lds_slots<LOGN, W>();
     __shared__ W lds_all[G::P * G::LW + NL * G::P * G::N];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped

@@ -35,27 +35,40 @@ namespace FHE_NS {
 constexpr int kPadA[17] = {0, 0, 0, 0, 0, 3, 3, 3, 4, 5, 5, 6, 7, 8, 5, 5, 0};
 constexpr int kPadB[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 10, 10, 0};
 
-template <int L>
+// Geometry key: log2(N) in bits 0-7, log2(coefficients per thread) in bits
+// 8-11 (0 = the default min(log2 N, 4)).  Every template below that takes
+// `int LOGN` accepts a key, so a kernel opts into 32 coefficients per thread
+// (radix-32 passes, N/32 threads) with gk(logn, 5).
+constexpr int gk(int logn, int loge) { return logn | (loge << 8); }
+constexpr int gk_logn(int k) { return k & 0xff; }
+constexpr int gk_loge(int k) { return (k >> 8) ? (k >> 8) : ((k & 0xff) < 4 ? (k & 0xff) : 4); }
+
+// Pads for 32 coefficients per thread (tools/lab/lds_pads.py): i + (i >> (L-5))
+// is conflict-free for every pass layout at L = 11..14.
+template <int K>
 __host__ __device__ constexpr uint32_t pad_idx(uint32_t i) {
-    return i + (kPadA[L] ? (i >> kPadA[L]) : 0u) + (kPadB[L] ? (i >> kPadB[L]) : 0u);
+    constexpr int L = gk_logn(K);
+    constexpr int A = gk_loge(K) == 5 ? 0 : kPadA[L];
+    constexpr int B = gk_loge(K) == 5 ? L - 5 : kPadB[L];
+    return i + (A ? (i >> A) : 0u) + (B ? (i >> B) : 0u);
 }
 // LDS words per polynomial
-template <int L>
-constexpr int lds_words() { return (int)pad_idx<L>((1u << L) - 1) + 1; }
+template <int K>
+constexpr int lds_words() { return (int)pad_idx<K>((1u << gk_logn(K)) - 1) + 1; }
 
 // ---------------------------------------------------------------- geometry
 template <int LOGN>
 struct Geo {
-    static constexpr int L = LOGN;
+    static constexpr int L = gk_logn(LOGN);
     static constexpr int N = 1 << L;
-    static constexpr int LOGE = L < 4 ? L : 4;
+    static constexpr int LOGE = gk_loge(LOGN);
     static constexpr int E = 1 << LOGE;
     static constexpr int LOGT = L - LOGE;
     static constexpr int T = 1 << LOGT;
     static constexpr int NP = (L + LOGE - 1) / LOGE;  // passes
     static constexpr int P = T >= 256 ? 1 : 256 / T;  // polynomials per workgroup
     static constexpr int THREADS = T * P;
-    static constexpr int LW = lds_words<L>();  // padded LDS words per polynomial
+    static constexpr int LW = lds_words<LOGN>();  // padded LDS words per polynomial
     static constexpr int S(int p) { return p * LOGE; }
     // Waves per SIMD the LDS footprint allows (160 KiB LDS, 2048 threads per
     // CU): used as __launch_bounds__' min-waves-per-EU so the register
@@ -74,6 +87,16 @@ struct Geo {
     }
     static constexpr int R(int p) { return (L - p * LOGE) < LOGE ? (L - p * LOGE) : LOGE; }
 };
+
+// Polynomial index within the workgroup.  P == 1 must be the constant 0:
+// otherwise the compiler cannot prove the polynomial's buffer resource
+// wave-uniform (threadIdx.x >> LOGT is 0 only because of the launch size)
+// and wraps every buffer access in a readfirstlane waterfall loop.
+template <typename G>
+__device__ __forceinline__ uint32_t wg_poly() {
+    if constexpr (G::P == 1) return 0u;
+    else return threadIdx.x >> G::LOGT;
+}
 
 __host__ __device__ constexpr uint32_t cbrv(uint32_t x, int bits) {
     uint32_t r = 0;
@@ -286,6 +309,68 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 
+// One stage (K) of a pass, forward (CT) / inverse (GS).
+template <int LOGN, int PASS, int K, bool LAZY, typename W>
+__device__ __forceinline__ void fwd_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                          const Arith<W> &ar) {
+    using P = PassTw<LOGN, PASS>;
+    constexpr int R = P::R, NU = P::NU;
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int tt = 0; tt < (1 << R); ++tt) {
+            if (tt & (1 << K)) continue;
+            const int e = tt + (u << R), e2 = e + (1 << K);
+            const Tw<W> w = t[P::slot(K, u, tt & ((1 << K) - 1))];
+            if constexpr (LAZY) ar.ct_lazy(v[e], v[e2], w);
+            else ar.ct(v[e], v[e2], w);
+        }
+}
+template <int LOGN, int PASS, int K, bool FOLD, typename W>
+__device__ __forceinline__ void inv_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                          const Arith<W> &ar, Tw<W> scale) {
+    using P = PassTw<LOGN, PASS>;
+    constexpr int S = P::S, R = P::R, NU = P::NU;
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int tt = 0; tt < (1 << R); ++tt) {
+            if (tt & (1 << K)) continue;
+            const int e = tt + (u << R), e2 = e + (1 << K);
+            if (FOLD && S + K == 0) ar.gs_scaled(v[e], v[e2], scale);
+            else ar.gs(v[e], v[e2], t[P::slot(K, u, tt & ((1 << K) - 1))]);
+        }
+}
+
+// Staged twiddles (32 coefficients per thread, where a pass holds 31 twiddle
+// pairs per slot group): the twiddles of stage K+LA are issued while stage K
+// computes (LA = the stages issued before the exchange), and a scheduling
+// barrier per stage stops the compiler from hoisting every load to the top
+// of the pass (which costs ~60 VGPRs and spills beside two 32-word spectra).
+template <int LOGN, int PASS, int K, int LOOK, bool LAZY, typename W>
+__device__ __forceinline__ void fwd_stages(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                           const Tw<W> *__restrict__ tw, const Arith<W> &ar) {
+    constexpr int R = PassTw<LOGN, PASS>::R;
+    if constexpr (K < R) {
+        if constexpr (K + LOOK < R) load_tw<LOGN, PASS, W, K + LOOK, K + LOOK + 1>(tau, tw, t);
+        fwd_stage<LOGN, PASS, K, LAZY>(v, t, ar);
+        __builtin_amdgcn_sched_barrier(0);
+        fwd_stages<LOGN, PASS, K + 1, LOOK, LAZY>(tau, v, t, tw, ar);
+    }
+}
+template <int LOGN, int PASS, int K, int LOOK, bool FOLD, typename W>
+__device__ __forceinline__ void inv_stages(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                           const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale) {
+    if constexpr (K >= 0) {
+        if constexpr (K - LOOK >= 0) load_tw<LOGN, PASS, W, K - LOOK, K - LOOK + 1>(tau, tw, t);
+        inv_stage<LOGN, PASS, K, FOLD>(v, t, ar, scale);
+        __builtin_amdgcn_sched_barrier(0);
+        inv_stages<LOGN, PASS, K - 1, LOOK, FOLD>(tau, v, t, tw, ar, scale);
+    }
+}
+template <int LOGN>
+constexpr bool staged_tw() { return Geo<LOGN>::LOGE >= 5; }
+
 // Passes PASS..NP-1 of the forward transform, exchanging through LDS.
 // hook() runs once, in the last pass after its twiddle loads are issued: the
 // place to start HBM loads for what follows the transform (VMEM counters
@@ -301,10 +386,54 @@ __device__ __forceinline__ void fwd_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
         lds_store<LOGN, PASS - 1>(lds, v, tau);
         __syncthreads();
         lds_load<LOGN, PASS>(lds, v, tau);
-        load_tw<LOGN, PASS, W, PF, 8>(tau, tw, t);
-        if constexpr (PASS == G::NP - 1) hook();
-        fwd_pass<LOGN, PASS, LAZY>(v, t, ar);
+        if constexpr (staged_tw<LOGN>()) {
+            // stages 0..PF-1 issued before the exchange; stage K issues K+PF
+            if constexpr (PASS == G::NP - 1) hook();
+            fwd_stages<LOGN, PASS, 0, PF, LAZY>(tau, v, t, tw, ar);
+        } else {
+            load_tw<LOGN, PASS, W, PF, 8>(tau, tw, t);
+            if constexpr (PASS == G::NP - 1) hook();
+            fwd_pass<LOGN, PASS, LAZY>(v, t, ar);
+        }
         fwd_rest<LOGN, PASS + 1, LAZY, PF>(lds, v, tau, tw, ar, hook);
+    }
+}
+
+// ---------------------------------------------------------------- dual
+// Two forward transforms in lockstep (polymul's fwd(a) and fwd(b)): every
+// twiddle is loaded once and applied to both, the butterflies of the two
+// are independent (twice the ILP of one transform), and no spectrum has to
+// be parked while the other runs.  One LDS exchange buffer serves both in
+// turn (store a / sync / load a / sync / store b / sync / load b).
+template <int LOGN, int PASS, int K, int LOOK, bool LAZY, typename W>
+__device__ __forceinline__ void fwd_stages2(uint32_t tau, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E],
+                                            Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT], const Tw<W> *__restrict__ tw,
+                                            const Arith<W> &ar) {
+    constexpr int R = PassTw<LOGN, PASS>::R;
+    if constexpr (K < R) {
+        if constexpr (K + LOOK < R) load_tw<LOGN, PASS, W, K + LOOK, K + LOOK + 1>(tau, tw, t);
+        fwd_stage<LOGN, PASS, K, LAZY>(v, t, ar);
+        fwd_stage<LOGN, PASS, K, LAZY>(v2, t, ar);
+        __builtin_amdgcn_sched_barrier(0);
+        fwd_stages2<LOGN, PASS, K + 1, LOOK, LAZY>(tau, v, v2, t, tw, ar);
+    }
+}
+template <int LOGN, int PASS, bool LAZY, int PF, typename W>
+__device__ __forceinline__ void fwd_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
+                                          const Tw<W> *__restrict__ tw, const Arith<W> &ar) {
+    using G = Geo<LOGN>;
+    if constexpr (PASS < G::NP) {
+        Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);
+        lds_store<LOGN, PASS - 1>(lds, v, tau);
+        __syncthreads();
+        lds_load<LOGN, PASS>(lds, v, tau);
+        __syncthreads();
+        lds_store<LOGN, PASS - 1>(lds, v2, tau);
+        __syncthreads();
+        lds_load<LOGN, PASS>(lds, v2, tau);
+        fwd_stages2<LOGN, PASS, 0, PF, LAZY>(tau, v, v2, t, tw, ar);
+        fwd_rest2<LOGN, PASS + 1, LAZY, PF>(lds, v, v2, tau, tw, ar);
     }
 }
 
@@ -321,8 +450,13 @@ __device__ __forceinline__ void inv_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
         lds_store<LOGN, PASS + 1>(lds, v, tau);
         __syncthreads();
         lds_load<LOGN, PASS>(lds, v, tau);
-        load_tw<LOGN, PASS, W, 0, KS>(tau, tw, t);
-        inv_pass<LOGN, PASS, FOLD>(v, t, ar, scale);
+        if constexpr (staged_tw<LOGN>()) {
+            // stages R-1..KS issued before the exchange; stage K issues K-PF
+            inv_stages<LOGN, PASS, R - 1, R - KS, FOLD>(tau, v, t, tw, ar, scale);
+        } else {
+            load_tw<LOGN, PASS, W, 0, KS>(tau, tw, t);
+            inv_pass<LOGN, PASS, FOLD>(v, t, ar, scale);
+        }
         inv_rest<LOGN, PASS - 1, FOLD, PF>(lds, v, tau, tw, ar, scale);
     }
 }
@@ -389,6 +523,42 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
     for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
 }
 
+#ifndef FHE_LOAD_INFLIGHT
+#define FHE_LOAD_INFLIGHT 1
+#endif
+// As load_coeffs, for 32 coefficients per thread: raw u64 words are 2 VGPRs
+// each, so only IN chunks of CH are in flight at once and each chunk is
+// narrowed before the next is issued (scheduling barriers keep the compiler
+// from hoisting all 32 loads, which spills beside a parked spectrum).
+template <int E, int CH, int IN, typename W, typename F>
+__device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, uint64_t q, uint64_t mu, F &&addr_of) {
+    constexpr int NC = E / CH;
+    uint64_t raw[E];
+#pragma unroll
+    for (int c = 0; c < IN && c < NC; ++c)
+#pragma unroll
+        for (int t = c * CH; t < c * CH + CH; ++t) raw[t] = addr_of(t);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (c + IN < NC) {
+#pragma unroll
+            for (int t = (c + IN) * CH; t < (c + IN) * CH + CH; ++t) raw[t] = addr_of(t);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bool bad = false;
+#pragma unroll
+        for (int t = c * CH; t < c * CH + CH; ++t) bad |= raw[t] >= lim;
+        if (__builtin_expect(bad, 0)) {
+#pragma unroll
+            for (int t = c * CH; t < c * CH + CH; ++t)
+                if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+        }
+#pragma unroll
+        for (int t = c * CH; t < c * CH + CH; ++t) v[t] = W(raw[t]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Forward transform of one polynomial held by this thread group: HBM load
 // (bit-reversed, coalesced), all passes; result left in v (last layout,
 // values in [0, 4q), or [0, (4+2L)q) when LAZY; every bound is <= R, so a
@@ -422,9 +592,9 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
     } else if constexpr (G::P == 1) {  // the caller has returned early if !valid
         const auto r = brsrc(src);
         const uint32_t vo = (tau << sh) * 8u;
-        load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
-            return bload(r, vo, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u);
-        });
+        auto at = [&](int t) -> uint64_t { return bload(r, vo, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u); };
+        if constexpr (G::LOGE == 5) load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, A.q64, A.mu64, at);
+        else load_coeffs<G::E>(v, lim, A.q64, A.mu64, at);
     } else {
         load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
             return valid ? __builtin_nontemporal_load(src + ((tau + cbrv(t, G::LOGE) * G::T) << sh)) : 0;
@@ -437,6 +607,43 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
     }
     fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
     fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar, hook);
+}
+
+// fwd_poly for two polynomials at once (P == 1, no sub-transform offsets):
+// results in v (from src) and v2 (from src2), last-pass layout.
+template <int LOGN, bool NEGA, bool LAZY, int PF, typename W>
+__device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
+                                          const uint64_t *__restrict__ src, const uint64_t *__restrict__ src2,
+                                          const NttArgs<W> &A) {
+    using G = Geo<LOGN>;
+    static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
+    Tw<W> t0[PassTw<LOGN, 0>::COUNT];
+    load_tw<LOGN, 0>(tau, A.twf, t0);
+    const uint64_t lim = NEGA ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
+    const uint32_t vo = tau * 8u;
+    {
+        const auto r = brsrc(src);
+        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+            return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
+        });
+    }
+    {
+        const auto r = brsrc(src2);
+        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v2, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+            return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
+        });
+    }
+    if constexpr (NEGA) {
+#pragma unroll
+        for (int t = 0; t < G::E; ++t) {
+            const Tw<W> tw = A.twist[tau + cbrv(t, G::LOGE) * G::T];
+            v[t] = A.ar.shoup(v[t], tw);
+            v2[t] = A.ar.shoup(v2[t], tw);
+        }
+    }
+    fwd_pass<LOGN, 0, LAZY, W>(v, t0, A.ar);
+    fwd_pass<LOGN, 0, LAZY, W>(v2, t0, A.ar);
+    fwd_rest2<LOGN, 1, LAZY, PF>(lds, v, v2, tau, A.twf, A.ar);
 }
 
 // Inverse transform from v (last-pass layout, values in [0, 2q)) to HBM

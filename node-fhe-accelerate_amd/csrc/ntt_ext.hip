@@ -97,7 +97,7 @@ k_dmac(DmArgs D, NttArgs<W> A) {
     constexpr int STASH = ext_stash<LOGN, W, K1, MODE>();
     constexpr int NIN = MODE == 1 ? 3 : K1;  // source polynomials per ciphertext
     __shared__ W lds_all[G::P * G::LW + ext_extra_words<LOGN, W, K1, MODE>()];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < D.batch;
     if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped

@@ -11,7 +11,7 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_wa
 k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::LW];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
@@ -44,7 +44,7 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
               size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::LW];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;

@@ -13,7 +13,7 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_wa
 k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::LW];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
@@ -52,17 +52,34 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 template <int LOGN, typename W>
 constexpr int polymul_stash() {
     using G = Geo<LOGN>;
-    if (LOGN < 5) return 0;
-    if (FHE_POLY_REG_STASH_14 && LOGN == 14 && sizeof(W) == 4) return 0;
-    if (FHE_POLY_HBM_STASH && LOGN == 14) return 2;
+    if (G::L < 5 || G::LOGE == 5) return 0;  // 32 coefficients per thread: fwd(a) stays in VGPRs
+    if (FHE_POLY_REG_STASH_14 && G::L == 14 && sizeof(W) == 4) return 0;
+    if (FHE_POLY_HBM_STASH && G::L == 14) return 2;
     return G::P * (G::LW + G::N) * (int)sizeof(W) <= 160 * 1024 ? 1 : 2;
 }
 template <int LOGN, typename W>
 constexpr int polymul_occ() {
     // with the stash in HBM the LDS footprint admits a second workgroup
-    if (polymul_stash<LOGN, W>() == 0 && LOGN >= 12) return Geo<LOGN>::template occ_waves<W>();
+    if (polymul_stash<LOGN, W>() == 0 && Geo<LOGN>::L >= 12) return Geo<LOGN>::template occ_waves<W>();
     return polymul_stash<LOGN, W>() == 2 && FHE_POLY_HBM_STASH ? Geo<LOGN>::template occ_waves<W>() : 1;
 }
+// Polymul geometry: at q < 2^30 and N >= 4096, 32 coefficients per thread
+// (radix-32 passes: 2 LDS exchanges per transform instead of 3, N/32 threads,
+// fwd(a) parked in VGPRs, conflict-free pads, two workgroups per CU so one's
+// HBM traffic overlaps the other's transforms).  FHE_POLY_E16=1: the 16-per-
+// thread kernel with the LDS stash (lab A/B).
+#ifndef FHE_POLY_E16
+#define FHE_POLY_E16 0
+#endif
+#ifndef FHE_PF_POLY32
+#define FHE_PF_POLY32 1
+#endif
+template <int LOGN, typename W>
+constexpr int polymul_key() {
+    return (!FHE_POLY_E16 && sizeof(W) == 4 && LOGN >= 13 && LOGN <= 14) ? gk(LOGN, 5) : LOGN;
+}
+template <int LOGN>
+constexpr int polymul_pf() { return Geo<LOGN>::LOGE == 5 ? FHE_PF_POLY32 : kPfPolymul; }
 
 template <int LOGN, typename W, bool NEGA, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
@@ -71,7 +88,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     using G = Geo<LOGN>;
     constexpr int STASH = polymul_stash<LOGN, W>();
     __shared__ W lds_all[G::P * G::LW + (STASH == 1 ? G::P * G::N : 0)];
-    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
     W *lds = lds_all + pl * G::LW;
@@ -88,7 +105,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     auto hook = [&] {
         if constexpr (PRE) load_raw<LOGN>(*reinterpret_cast<uint64_t(*)[G::E]>(rb), tau, b + poly * G::N);
     };
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tau, a + poly * G::N, valid, A, 0, 0, hook);
+    fwd_poly<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, tau, a + poly * G::N, valid, A, 0, 0, hook);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const W x = fwd_to_canon<LAZY>(v[e], A);  // canonical: times a raw output below
@@ -97,6 +114,10 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
         else if constexpr (STASH == 1) st[gi] = x;
         else if (valid) reinterpret_cast<W *>(crow)[gi] = x;  // W-typed: first half of c's row
     }
+    // keep b's raw loads (2 VGPRs per coefficient) out of the stash
+    // conversion (a 64-bit mad result per coefficient): interleaved, the two
+    // peak together and spill at 32 coefficients per thread
+    if constexpr (G::LOGE == 5) __builtin_amdgcn_sched_barrier(0);
     if constexpr (G::NP > 1) __syncthreads();  // LDS exchange buffer is reused by the second transform
     // opaque copy of the lane index (u64 path): stops the compiler from
     // keeping the first transform's address arithmetic live for reuse.  At
@@ -104,10 +125,10 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     uint32_t tb = tau;
     if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(tb));
     if constexpr (PRE)
-        fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A, 0, 0, NoHook{},
+        fwd_poly<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, tb, b + poly * G::N, valid, A, 0, 0, NoHook{},
                                                reinterpret_cast<uint64_t(*)[G::E]>(rb));
     else
-        fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tb, b + poly * G::N, valid, A);
+        fwd_poly<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, tb, b + poly * G::N, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tb, e);
@@ -120,7 +141,33 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     if constexpr (G::NP > 1) __syncthreads();
     uint32_t ti = tau;
     if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(ti));
-    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, ti, crow, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, NEGA, polymul_pf<LOGN>()>(lds, v, ti, crow, valid, A, A.ninv_r, A.untwist_r);
+}
+
+// Polymul with 32 coefficients per thread: fwd(a) and fwd(b) run in
+// lockstep (fwd_poly2: shared twiddles, two independent butterfly streams),
+// then the pointwise Montgomery product and the inverse.  Two workgroups per
+// CU (one 64 KiB exchange buffer each), so one's HBM traffic overlaps the
+// other's transforms.
+#ifndef FHE_POLY_DUAL
+#define FHE_POLY_DUAL 1
+#endif
+template <int LOGN, typename W, bool NEGA, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
+           NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    static_assert(G::P == 1, "one polynomial pair per workgroup");
+    __shared__ W lds[G::LW];
+    const uint32_t tau = threadIdx.x;
+    const size_t poly = blockIdx.x;
+    if (poly >= batch) return;
+    W v[G::E], vb[G::E];
+    fwd_poly2<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, vb, tau, a + poly * G::N, b + poly * G::N, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) v[e] = A.ar.mont(fwd_to_canon<LAZY>(v[e], A), vb[e]);  // canonical x raw (< R)
+    __syncthreads();  // the exchange buffer still holds b's last layout reads
+    inv_poly_from_regs<LOGN, NEGA, polymul_pf<LOGN>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r, A.untwist_r);
 }
 
 template <int LOGN, typename W, bool NEGA>
@@ -130,11 +177,23 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
     const size_t blocks = (batch + G::P - 1) / G::P;
     bool lazy = false;
     if constexpr (sizeof(W) == 4) lazy = p.lazy;
+    constexpr int PK = polymul_key<LOGN, W>();
+    using GP = Geo<PK>;
+    const size_t pblocks = (batch + GP::P - 1) / GP::P;
+    if constexpr (GP::LOGE == 5 && FHE_POLY_DUAL && sizeof(W) == 4) {
+        if (b) {
+            if (lazy)
+                hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+            else
+                hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+            return hipGetLastError();
+        }
+    }
     if (b && lazy) {
         if constexpr (sizeof(W) == 4)
-            hipLaunchKernelGGL((k_polymul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, s, a, b, c, batch, A);
+            hipLaunchKernelGGL((k_polymul<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
     } else if (b)
-        hipLaunchKernelGGL((k_polymul<LOGN, W, NEGA, false>), dim3(blocks), dim3(G::THREADS), 0, s, a, b, c, batch, A);
+        hipLaunchKernelGGL((k_polymul<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
     else
         hipLaunchKernelGGL((k_ntt_inv<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, c, batch, A);
     return hipGetLastError();
