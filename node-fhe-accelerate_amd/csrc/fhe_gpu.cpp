@@ -1130,6 +1130,13 @@ int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, co
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 
+// Largest batch the single-launch blind rotation takes.  Measured on MI355X
+// (tfhe-128-fast shape, q = 62-bit prime): batch 64 6.8 ms vs 39.2 ms per-step
+// launches, batch 8192 103 ms vs 184 ms -- it wins at every size, so the
+// per-step path only serves unsupported shapes and
+// FHE_BR_PERSIST_MAX=0.
+constexpr size_t kBrPersistMax = ~(size_t)0;
+
 int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
                            const uint64_t *lwe_a, const uint64_t *lwe_b, uint64_t lwe_q, const uint64_t *bsk_ntt,
                            uint64_t *acc, size_t batch, int where) {
@@ -1147,6 +1154,16 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
     FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
     FHE_TRY(hs.map(where, acc, bytes, 3));
+    // The whole loop as one launch with the accumulators in LDS
+    // (ntt_br.hip); FHE_BR_PERSIST_MAX caps the batch it takes (0 = never).
+    const char *pm = std::getenv("FHE_BR_PERSIST_MAX");
+    const size_t persist_max = pm ? (size_t)std::strtoull(pm, nullptr, 10) : kBrPersistMax;
+    if (lwe_dim > 0 && batch <= persist_max && FHE_NS::br_persist_supported(c->plan, (int)k + 1)) {
+        HIP_TRY(FHE_NS::launch_br_persist(c->plan, (int)k + 1, (int)level, (int)base_log, acc, bsk_ntt, lwe_a, lwe_b,
+                                          lwe_dim, lwe_q, batch),
+                "blind rotate kernel");
+        return where == FHE_HOST ? hs.finish() : FHE_OK;
+    }
     std::lock_guard<std::mutex> lk(c->br_mu);
     if (c->br_tmp_bytes < bytes) {
         if (c->br.exec) { (void)hipGraphExecDestroy(c->br.exec); c->br.exec = nullptr; }

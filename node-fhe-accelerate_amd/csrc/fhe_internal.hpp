@@ -49,6 +49,14 @@ hipError_t launch_relin(const Plan &p, int level, int base_log, const uint64_t *
 hipError_t launch_cmux_rotate(const Plan &p, int k1, int level, int base_log, const uint64_t *acc_in,
                               const uint64_t *ggsw, uint64_t *acc_out, size_t batch, const uint64_t *lwe_a,
                               uint32_t lwe_dim, uint32_t step, uint64_t lwe_q);
+// The whole blind rotation (initial X^-round(b 2N/q) rotation + lwe_dim
+// CMux steps) of a small batch in ONE launch (ntt_br.hip): one workgroup per
+// ciphertext, accumulators resident in LDS across all steps.  k1 == 2 and
+// 512 <= N <= 2048 only (br_persist_supported); acc is updated in place.
+bool br_persist_supported(const Plan &p, int k1);
+hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
+                             const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q,
+                             size_t batch);
 // CMux(ggsw, ct0, ct1) = ct0 + ggsw (x) (ct1 - ct0)
 hipError_t launch_cmux(const Plan &p, int k1, int level, int base_log, const uint64_t *ggsw, const uint64_t *ct0,
                        const uint64_t *ct1, uint64_t *out, size_t batch);

@@ -1,0 +1,174 @@
+// ntt_br.hip -- low-latency blind rotation (BootstrapEngine::blind_rotate,
+// bootstrap_engine.cpp:547-577: the initial rotation by -round(b 2N / q),
+// then for every LWE mask coefficient a_i the CMux step
+//   rot = (int32)((a_i * 2N + q/2) / q);  rot == 0: skip
+//   acc = acc + ExtProd(X^rot * acc - acc, bsk[i])          (cmux :520-540)
+// as ONE launch for the whole loop.
+//
+// The multi-launch path (k_dmac MODE 2, one launch per step over the batch,
+// one wave per ciphertext) is throughput-shaped: at batch 64 it leaves the
+// chip nearly idle and every step is the latency of 4 dependent transforms
+// by a single wave, plus an HBM/L2 round trip of the accumulators.  Here one
+// workgroup owns one ciphertext for all steps:
+//   * the (k+1) = 2 accumulators live in LDS (raw u64, exactly the values the
+//     multi-launch path would hold in HBM between steps);
+//   * the two digit polynomials of a decomposition level are transformed in
+//     parallel, each by 128 threads with N/128 coefficients per thread
+//     (geometry gk(logN, logN - 7): P = 2 polynomials per workgroup);
+//   * the MAC with the step's GGSW (NTT x R, Montgomery) accumulates in
+//     registers; the two halves swap their cross terms through LDS, so half j
+//     ends holding output component j and inverts it;
+//   * the inverse's epilogue adds the old accumulator (mod_add) back into LDS.
+// Same arithmetic as MODE 2 (digit load, red_q / subq / addq, Montgomery MAC,
+// canonical inverse), so results are bit-identical to the multi-launch path
+// and to the oracle.
+#include "fhe_internal.hpp"
+#include "lwe_ops.hpp"
+
+namespace FHE_NS {
+
+struct BrArgs {
+    uint64_t *acc;          // [batch][2][N], in/out
+    const uint64_t *bsk;    // [lwe_dim][2L][2][N] prepared GGSWs
+    const uint64_t *lwe_a;  // [batch][lwe_dim]
+    const uint64_t *lwe_b;  // [batch]
+    uint64_t lwe_q;
+    uint32_t lwe_dim;
+    int level, base_log;
+};
+
+template <int LOGN>
+constexpr int br_key() { return gk(LOGN, LOGN - 7); }
+
+template <int LOGN, typename W, bool NEGA>
+__global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
+    constexpr int K = br_key<LOGN>();
+    using G = Geo<K>;
+    static_assert(G::P == 2 && G::THREADS == 256, "two 128-thread halves per workgroup");
+    constexpr int N = G::N;
+    __shared__ uint64_t accs[2][N];   // raw accumulators (component j)
+    __shared__ W xlds[2 * G::LW];     // NTT exchange, one region per half
+    __shared__ W xbuf[2][N];          // cross-half MAC terms
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t ct = blockIdx.x;
+    const uint64_t q = A.q64, mu = A.mu64;
+    W *lds = xlds + pl * G::LW;
+    uint64_t *gacc = D.acc + ct * 2 * N;
+    {
+        // acc <- X^-round(b 2N/q) acc   (k_rotate's map)
+        const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
+        for (uint32_t i = threadIdx.x; i < 2u * N; i += G::THREADS) {
+            const uint32_t j = i / N, p = i % N;
+            accs[j][p] = rotated_at(gacc + (size_t)j * N, p, r0, N, q, mu);
+        }
+    }
+    __syncthreads();
+    const int level = D.level;
+    const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    const size_t ggsw_words = (size_t)2 * level * 2 * N;
+    const uint64_t *lwe_a = D.lwe_a + ct * D.lwe_dim;
+    for (uint32_t step = 0; step < D.lwe_dim; ++step) {
+        const int32_t r = rot_amount(lwe_a[step], N, D.lwe_q);  // workgroup-uniform
+        if (r == 0) continue;
+        const uint32_t rot = rot_norm(r, N);
+        const uint64_t *key = D.bsk + ggsw_words * step;
+        W oacc[G::E];
+        for (int g = 0; g < level; ++g) {
+            // row (pl, g): digit g of X^rot acc_pl - acc_pl (MSB digit first)
+            const int row = pl * level + g;
+            const uint32_t shift = uint32_t(level - 1 - g) * uint32_t(D.base_log);
+            // this row's key terms for both output components, in flight
+            // across the transform
+            uint64_t kv[2][G::E];
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const uint32_t gi = gidx<K, G::NP - 1>(tau, e);
+                kv[0][e] = key[((size_t)row * 2 + pl) * N + gi];
+                kv[1][e] = key[((size_t)row * 2 + (1 - pl)) * N + gi];
+            }
+            uint32_t tr = tau;
+            asm volatile("" : "+v"(tr));
+            W v[G::E];
+            Tw<W> t0[PassTw<K, 0>::COUNT];
+            load_tw<K, 0>(tr, A.twf, t0);
+            const uint64_t *ac = accs[pl];
+            load_coeffs<G::E>(v, (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
+                const uint32_t p = tr + cbrv(t, G::LOGE) * G::T;
+                const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
+                const uint64_t xr = j < (uint32_t)N ? ac[j] : red_q(q - ac[j - N], q, mu);
+                const uint64_t c = subq(red_q(xr, q, mu), red_q(ac[p], q, mu), q);
+                uint64_t d = (c >> shift) & mask;
+                if (d > half) d = red_q(q - (base - d), q, mu);
+                return d;
+            });
+            if constexpr (NEGA) {
+#pragma unroll
+                for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tr + cbrv(t, G::LOGE) * G::T]);
+            }
+            fwd_pass<K, 0, false>(v, t0, A.ar);
+            fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
+            // raw output (< 4q) times a canonical key: a valid Montgomery pair
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const uint32_t gi = gidx<K, G::NP - 1>(tr, e);
+                const W own = A.ar.mont(v[e], (W)kv[0][e]);
+                xbuf[1 - pl][gi] = A.ar.mont(v[e], (W)kv[1][e]);
+                oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) oacc[e] = A.ar.red2q(oacc[e] + xbuf[pl][gidx<K, G::NP - 1>(tr, e)]);
+            __syncthreads();  // xbuf and the exchange regions are reused
+        }
+        // component pl: inverse, then acc_pl = mod_add(inv, red_q(acc_pl))
+        uint32_t ti = tau;
+        asm volatile("" : "+v"(ti));
+        uint64_t *ap = accs[pl];
+        inv_poly_from_regs<K, NEGA, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, A.untwist, 0, 0,
+                                                      [&](uint32_t gi, uint64_t x) -> uint64_t {
+                                                          ap[gi] = addq(x, red_q(ap[gi], q, mu), q);
+                                                          return 0;
+                                                      });
+        __syncthreads();
+    }
+    for (uint32_t i = threadIdx.x; i < 2u * N; i += G::THREADS) gacc[i] = accs[i / N][i % N];
+}
+
+bool br_persist_supported(const Plan &p, int k1) { return k1 == 2 && p.logn >= 9 && p.logn <= 11; }
+
+template <int LOGN, typename W, bool NEGA>
+static hipError_t br_one(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
+    hipLaunchKernelGGL((k_br_persist<LOGN, W, NEGA>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+    return hipGetLastError();
+}
+template <typename W, bool NEGA>
+static hipError_t br_dispatch(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
+    switch (p.logn) {
+    case 9: return br_one<9, W, NEGA>(p, D, batch, A);
+    case 10: return br_one<10, W, NEGA>(p, D, batch, A);
+    case 11: return br_one<11, W, NEGA>(p, D, batch, A);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
+                             const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q,
+                             size_t batch) {
+    if (!br_persist_supported(p, k1)) return hipErrorInvalidValue;
+    if (batch == 0) return hipSuccess;
+    // grid.x <= 2^31 - 1 workgroups
+    const size_t per = (size_t)1 << 30;
+    for (size_t b0 = 0; b0 < batch; b0 += per) {
+        const size_t nb = batch - b0 < per ? batch - b0 : per;
+        BrArgs D{acc + b0 * 2 * ((size_t)1 << p.logn), bsk, lwe_a + b0 * lwe_dim, lwe_b + b0, lwe_q, lwe_dim, level,
+                 base_log};
+        hipError_t e = p.word == 32 ? (p.nega ? br_dispatch<uint32_t, true>(p, D, nb, p.a32)
+                                              : br_dispatch<uint32_t, false>(p, D, nb, p.a32))
+                                    : (p.nega ? br_dispatch<uint64_t, true>(p, D, nb, p.a64)
+                                              : br_dispatch<uint64_t, false>(p, D, nb, p.a64));
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace FHE_NS

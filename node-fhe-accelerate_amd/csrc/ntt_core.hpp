@@ -45,11 +45,20 @@ constexpr int gk_loge(int k) { return (k >> 8) ? (k >> 8) : ((k & 0xff) < 4 ? (k
 
 // Pads for 32 coefficients per thread (tools/lab/lds_pads.py): i + (i >> (L-5))
 // is conflict-free for every pass layout at L = 11..14.
+// Fewer coefficients per thread (the low-latency blind rotation,
+// ntt_br.hip) at N = 1024 with 64-bit words: (5, 6) for 8 per thread, (4, 5)
+// for 4 (lds_pads.py --u64); other degrees take the 16-per-thread pads.
+constexpr int pad_a(int L, int E) {
+    return E == 5 ? 0 : (L == 10 && E == 3) ? 5 : (L == 10 && E == 2) ? 4 : kPadA[L];
+}
+constexpr int pad_b(int L, int E) {
+    return E == 5 ? L - 5 : (L == 10 && E == 3) ? 6 : (L == 10 && E == 2) ? 5 : kPadB[L];
+}
 template <int K>
 __host__ __device__ constexpr uint32_t pad_idx(uint32_t i) {
     constexpr int L = gk_logn(K);
-    constexpr int A = gk_loge(K) == 5 ? 0 : kPadA[L];
-    constexpr int B = gk_loge(K) == 5 ? L - 5 : kPadB[L];
+    constexpr int A = pad_a(L, gk_loge(K));
+    constexpr int B = pad_b(L, gk_loge(K));
     return i + (A ? (i >> A) : 0u) + (B ? (i >> B) : 0u);
 }
 // LDS words per polynomial
@@ -500,7 +509,10 @@ __device__ __forceinline__ void coeffs_from_raw(W (&v)[E], uint64_t (&raw)[E], u
     if (__builtin_expect(bad, 0)) {
 #pragma unroll
         for (int t = 0; t < E; ++t)
-            if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+            {
+                if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+                __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time (no spills)
+            }
     }
 #pragma unroll
     for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
@@ -517,7 +529,10 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
     if (__builtin_expect(bad, 0)) {
 #pragma unroll
         for (int t = 0; t < E; ++t)
-            if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+            {
+                if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+                __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time (no spills)
+            }
     }
 #pragma unroll
     for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
@@ -551,7 +566,10 @@ __device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, uin
         if (__builtin_expect(bad, 0)) {
 #pragma unroll
             for (int t = c * CH; t < c * CH + CH; ++t)
+                {
                 if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
+                __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time (no spills)
+            }
         }
 #pragma unroll
         for (int t = c * CH; t < c * CH + CH; ++t) v[t] = W(raw[t]);

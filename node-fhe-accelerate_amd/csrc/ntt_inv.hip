@@ -188,14 +188,19 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
                 hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
             return hipGetLastError();
         }
+    } else {
+        if (b && lazy) {
+            if constexpr (sizeof(W) == 4)
+                hipLaunchKernelGGL((k_polymul<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+            return hipGetLastError();
+        } else if (b) {
+            hipLaunchKernelGGL((k_polymul<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+            return hipGetLastError();
+        }
     }
-    if (b && lazy) {
-        if constexpr (sizeof(W) == 4)
-            hipLaunchKernelGGL((k_polymul<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
-    } else if (b)
-        hipLaunchKernelGGL((k_polymul<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
-    else
+    {
         hipLaunchKernelGGL((k_ntt_inv<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, c, batch, A);
+    }
     return hipGetLastError();
 }
 

@@ -179,6 +179,39 @@ def test_blind_rotate_vs_oracle(fg, n, q, bl, lv, dim):
         assert (acc[i] == exp).all(), i
 
 
+@pytest.mark.parametrize("n,q,bl,lv,mode", [(512, 12289, 4, 3, "compat"), (1024, P62, 23, 1, "compat"),
+                                            (1024, P27, 9, 3, "negacyclic"), (1024, P62, 15, 2, "negacyclic"),
+                                            (2048, P62, 23, 1, "compat"), (2048, 40961, 5, 2, "compat")])
+def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q, bl, lv, mode):
+    """Small batches take the single-launch blind rotation (ntt_br.hip,
+    accumulators in LDS for the whole loop); FHE_BR_PERSIST_MAX=0 forces the
+    per-step launches.  Both bit-exact with each other, and rows vs the
+    oracle (compat mode)."""
+    k, b, dim = 1, 5, 24
+    r = fg.PolynomialRing(n, q, mode=mode)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(71 + n, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a = rnd(72, q, b, dim)
+    lwe_a[0, :3] = [0, q - 1, 1]   # skipped step, rotation 2N, tiny rotation
+    lwe_a[1, :] = 0                 # all steps skipped
+    lwe_b = rnd(73, q, b)
+    acc0 = rnd(74, q, b, k + 1, n)  # both components non-zero
+    acc0[2, 0, :3] = [2**64 - 1, q, q + 1]  # raw words
+    got = {}
+    for pmax in ("4096", "0"):
+        monkeypatch.setenv("FHE_BR_PERSIST_MAX", pmax)
+        acc = acc0.copy()
+        be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
+        got[pmax] = acc
+    assert (got["4096"] == got["0"]).all()
+    if mode == "compat":
+        t = oracle.NTT(n, q)
+        for i in (0, 1, 2):
+            exp = t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])
+            assert (got["4096"][i] == exp).all(), i
+
+
 def test_sample_extract_vs_oracle(fg):
     n, q, k = 1024, P27, 1
     r = fg.PolynomialRing(n, q)

@@ -80,7 +80,10 @@ def test_golden_large(fg, golden_dir):
 CONFIGS = [(4, 17), (8, 17), (16, 97), (32, 193), (64, 257), (128, 769), (256, 7681), (512, 12289),
            (1024, P27), (1024, P62), (2048, 40961), (4096, P27), (4096, P62), (8192, P27), (8192, P62),
            (16384, P27), (16384, P62), (1024, 1152921504606584833), (2048, 1073479681),
-           (32768, P27), (32768, P62), (65536, P27), (65536, P62)]
+           (32768, P27), (32768, P62), (65536, P27), (65536, P62),
+           # q in (2^27, 2^30): 32-bit lanes without the lazy forward (the
+           # 32-coefficient polymul's non-lazy instantiation at N=8192/16384)
+           (8192, 1073643521), (16384, 1073643521)]
 
 
 @pytest.mark.parametrize("n,q", CONFIGS)
@@ -175,6 +178,35 @@ def test_round_trip_full_config_sizes(fg):
         t = oracle.NTT(n, q)
         xs = x[rows].cpu().numpy().view(np.uint64)
         assert (f[rows].cpu().numpy().view(np.uint64) == t.forward(xs)).all()
+
+
+def test_full_c3_batch_rows_vs_oracle(fg):
+    """The bench workload itself (BASELINE configs[2], C3): N=16384, batch
+    65536, q=132120577 -- 8 GiB per operand, every launch over the whole
+    batch.  First, middle and last rows of forward NTT + modmul and of the
+    polymul (C4) bit-exact against the oracle; the rest by a property
+    (fwd_mul against an independent forward NTT then pointwise product)."""
+    import torch
+
+    n, q, b = 16384, P27, 65536
+    r = fg.PolynomialRing(n, q)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a = torch.randint(0, q, (b, n), device="cuda", dtype=torch.int64, generator=g)
+    w = torch.randint(0, q, (b, n), device="cuda", dtype=torch.int64, generator=g)
+    out = torch.empty_like(a)
+    rows = [0, 1, b // 2, b - 2, b - 1]
+    t = oracle.NTT(n, q)
+    xa, xw = a[rows].cpu().numpy().view(np.uint64), w[rows].cpu().numpy().view(np.uint64)
+    r.forward_ntt_mul(a, w, out=out)
+    assert (out[rows].cpu().numpy().view(np.uint64) == t.fwd_mul(xa, xw)).all()
+    # whole batch: fwd_mul == pointwise(fwd(a), w) (an independent kernel pair)
+    f = r.forward_ntt(a[: b // 8])
+    assert torch.equal(out[: b // 8], r.pointwise_multiply(f, w[: b // 8]))
+    del f
+    r.multiply(a, w, out=out)
+    assert (out[rows].cpu().numpy().view(np.uint64) == t.polymul(xa, xw)).all()
+    del a, w, out
+    torch.cuda.empty_cache()
 
 
 def test_large_degree_chunk_boundaries(fg):
@@ -322,7 +354,7 @@ def test_negacyclic_mode_is_ring_product(fg, golden_dir):
         assert L(r.multiply(U(c["x"]), U(c["y"]))) == c["product"]
     # larger: schoolbook via the oracle's exact integer arithmetic is too slow,
     # check the convolution identity x * X == shift with sign
-    for n, q in ((4096, P62), (16384, P27), (32768, P62), (65536, P27)):
+    for n, q in ((4096, P62), (8192, P27), (16384, P27), (16384, 1073643521), (32768, P62), (65536, P27)):
         r = fg.PolynomialRing(n, q, mode="negacyclic")
         x = oracle.splitmix_fill(3, q, n).reshape(1, n)
         X = np.zeros((1, n), np.uint64)

@@ -8,7 +8,7 @@ busy bank adds one cycle.  Element i lives at word pad(i) = i + (i>>A) + (i>>B)
 [+ (i>>C)].  Pass p of a transform owns, per lane tau and slot group u, the
 elements lay(g) | (t << S), t < 2^R, g = brv(tau) (pass 0) or tau + u*T.
 
-usage: lds_pads.py LOGN LOGE [--eval A B [C]]
+usage: lds_pads.py LOGN LOGE [--u64] [--eval A B [C]]
 """
 import itertools
 import sys
@@ -50,38 +50,44 @@ def patterns(L, LE):
     return out
 
 
-def cost(pats, pads, T):
+def cost(pats, pads, T, wide=False):
+    """wide: 8-byte words (ds_read_b64: 32-lane groups, 64 banks; ds_write_b64:
+    16-lane groups, 32 banks; each access covers two consecutive dwords)."""
     def pad(i):
         return i + sum(i >> a for a in pads if a)
 
     extra = 0
+    groups = ((32, 64), (16, 32)) if wide else ((32, 32),)
     for insts in pats:
         for els in insts:
-            for w0 in range(0, T, 64):
-                for g0 in (w0, w0 + 32):
-                    lanes = els[g0:g0 + 32]
+            for gsz, nb in groups:
+                for g0 in range(0, T, gsz):
+                    lanes = els[g0:g0 + gsz]
                     if not lanes:
                         continue
                     banks = {}
                     for e in lanes:
-                        banks.setdefault(pad(e) % 32, set()).add(pad(e))
+                        dw = 2 * pad(e) if wide else pad(e)
+                        for d in ((dw, dw + 1) if wide else (dw,)):
+                            banks.setdefault(d % nb, set()).add(d)
                     extra += max(len(s) for s in banks.values()) - 1
     return extra
 
 
 def main():
     L, LE = int(sys.argv[1]), int(sys.argv[2])
+    wide = "--u64" in sys.argv
     T, NP, Rs, LE = geo(L, LE)
     pats = patterns(L, LE)
     if "--eval" in sys.argv:
-        pads = [int(x) for x in sys.argv[sys.argv.index("--eval") + 1:]]
-        print("pads", pads, "extra cycles per (all passes store+load once):", cost(pats, pads, T))
+        pads = [int(x) for x in sys.argv[sys.argv.index("--eval") + 1:] if not x.startswith("--")]
+        print("pads", pads, "extra cycles per (all passes store+load once):", cost(pats, pads, T, wide))
         return
     res = []
     for A, B in itertools.combinations_with_replacement(range(0, L + 1), 2):
         if A and B and A == B:
             continue
-        res.append((cost(pats, [A, B], T), A, B))
+        res.append((cost(pats, [A, B], T, wide), A, B))
     res.sort()
     for r in res[:12]:
         words = (1 << L) - 1 + sum(((1 << L) - 1) >> a for a in r[1:] if a) + 1

@@ -8,7 +8,7 @@ for f in sys.argv[1:]:
     s = json.load(open(f))
     p = s["pmc_per_launch_avg"]
     w = p["SQ_WAVE_CYCLES"]
-    ns = float(s["kernel_stats"][0]["AverageNs"])
+    ns = float(s.get("kernel_avg_ns") or s["kernel_stats"][0]["AverageNs"])
     clk = p.get("GRBM_GUI_ACTIVE", 0) / 8 / (ns * 1e-9) / 1e9
     print(f, f"{ns / 1e6:.3f} ms vgpr {s.get('vgpr')} clk {clk:.2f} GHz")
     print("  per wave:", {k[3:]: round(v / p["SQ_WAVES"]) for k, v in p.items() if k.startswith("SQ_") and k != "SQ_WAVES"})

@@ -41,6 +41,13 @@ def main():
             {k: (r[k][:160] if k == "Name" else r[k]) for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
             for r in rows[:8]
         ]
+        # the kernel this summary is about (kernel_stats is sorted by total
+        # time, so its first row can be another kernel of the same run)
+        mine = [r for r in rows if ksub in r["Name"]]
+        if mine:
+            top = max(mine, key=lambda r: float(r["TotalDurationNs"]) if "TotalDurationNs" in r else float(r["AverageNs"]))
+            out["kernel_stats_name"] = top["Name"][:160]
+            out["kernel_avg_ns"] = float(top["AverageNs"])
     per_counter = defaultdict(list)
     grid = {}
     for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
