@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--only", default="", help="run only this kernel (fwd_mul|polymul|fwd|inv) for profiling")
     ap.add_argument("--no-check", action="store_true", help="skip the oracle spot check (profiling runs)")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-resident (FHE_HOST, PCIe) measurement")
+    ap.add_argument("--only-host", action="store_true", help="only the host-resident measurement (lab)")
     ap.add_argument("--no-cipher", dest="cipher", action="store_false",
                     help="skip the ciphertext-level side metrics (ct multiply, relinearize, blind rotate)")
     return ap.parse_args()
@@ -186,6 +188,51 @@ def time_gather(dist, out, n, polys=4096):
     nbytes = g * n * 8 * world
     return {"backend": dist.get_backend(), "polys_per_rank": g, "bytes_into_root": nbytes, "ms": ms,
             "GBps_into_root": nbytes / (ms * 1e-3) / 1e9}
+
+
+def host_resident(fhe_gpu, n, q, polys=8192, reps=3):
+    """SURVEY.md 8(d) / BASELINE.md section 2: the FHE_HOST path (what the
+    N-API addon hands over: pageable host arrays in, host array out), timed
+    end to end -- H2D + kernel + D2H, pipelined over pinned staging slots
+    (fhe_gpu.cpp staged()).  Never `value`.  Also the raw pageable H2D / D2H
+    copy rates on this box (torch), for the PCIe bound."""
+    ring = fhe_gpu.PolynomialRing(n, q, device=torch.cuda.current_device())
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, q, size=(polys, n), dtype=np.uint64)
+    w = rng.integers(0, q, size=(polys, n), dtype=np.uint64)
+    o = np.empty_like(a)
+    ring.forward_ntt_mul(a[:64], w[:64], out=o[:64])  # warm-up (staging buffers)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ring.forward_ntt_mul(a, w, out=o)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    moved = 24 * n * polys  # a, w in; out back
+    res = {"polys": polys, "n": n, "q": q, "ntt_per_s": polys / best, "ms": best * 1e3,
+           "pcie_GBs_moved": moved / best / 1e9, "bytes_per_ntt": 24 * n}
+    # raw copy rates, pageable host memory (as the FHE_HOST caller has it)
+    x = torch.from_numpy(a.view(np.int64))
+    d = torch.empty(x.shape, dtype=torch.int64, device="cuda")
+    d.copy_(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d.copy_(x)
+    torch.cuda.synchronize()
+    h2d = x.numel() * 8 / (time.perf_counter() - t0) / 1e9
+    t0 = time.perf_counter()
+    x.copy_(d)
+    torch.cuda.synchronize()
+    d2h = x.numel() * 8 / (time.perf_counter() - t0) / 1e9
+    res["h2d_pageable_GBs"], res["d2h_pageable_GBs"] = h2d, d2h
+    # bound: 16N bytes in and 8N out per NTT, the two directions overlapped
+    res["pcie_bound_ntt_per_s"] = min(h2d * 1e9 / (16 * n), d2h * 1e9 / (8 * n))
+    res["frac_of_pcie_bound"] = res["ntt_per_s"] / res["pcie_bound_ntt_per_s"]
+    ok = bool((o[[0, polys - 1]] == __import__("oracle").NTT(n, q).fwd_mul(a[[0, polys - 1]], w[[0, polys - 1]])).all())
+    res["parity_ok"] = ok
+    del d
+    torch.cuda.empty_cache()
+    return res
 
 
 def _spot_check(ring, a, b, out, n, q, batch):
@@ -392,6 +439,10 @@ def main():
 
     n, B, K, W = args.n, args.batch, args.steps, args.warmup
     extra = {}
+    if args.only_host:
+        if rank == 0:
+            print(json.dumps({"host_resident": host_resident(fhe_gpu, n, args.q)}), flush=True)
+        return
     if args.only in ("ct_mul", "relin", "blind_rotate", "c5", "c2"):  # profiling runs of the side metrics
         c = cipher_workload(fhe_gpu, K, W, dist, args.only)
         if rank == 0:
@@ -409,6 +460,8 @@ def main():
         }
     if args.cipher and not args.only:
         extra["cipher"] = cipher_workload(fhe_gpu, max(3, K // 4), 1, dist)
+    if rank == 0 and not args.only and not args.no_host:
+        extra["host_resident"] = host_resident(fhe_gpu, n, args.q)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()

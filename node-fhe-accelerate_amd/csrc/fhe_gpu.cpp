@@ -96,9 +96,19 @@ struct fhe_ctx {
     Tables tab;
     FHE_NS::Plan plan{};
     std::vector<u64> fwd_tw, inv_tw;  // reference twiddle vectors (host copy)
+    // host staging pipeline of the FHE_HOST batch calls (staged()): kSlots
+    // slots, each a stream, pinned host buffers and device buffers for two
+    // inputs and one output, so that the host copy of chunk k+1, the H2D of
+    // k+1, the kernel of k and the D2H of k-1 overlap
+    struct Pipe {
+        static constexpr int kSlots = 3;
+        hipStream_t st[kSlots] = {};
+        hipEvent_t done[kSlots] = {};
+        void *pin[kSlots][3] = {};
+        void *dev[kSlots][3] = {};
+        size_t bytes = 0;  // per buffer
+    } pipe;
     std::mutex scratch_mu;
-    void *scratch[3] = {nullptr, nullptr, nullptr};
-    size_t scratch_bytes = 0;
     // blind rotation: ping-pong accumulator buffer and the captured launch
     // sequence (1 rotation + lwe_dim CMux steps + copy) as a hipGraph, reused
     // while the call's buffers and shape are unchanged
@@ -209,13 +219,29 @@ int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
     return FHE_OK;
 }
 
+void free_pipe(fhe_ctx *c) {
+    auto &P = c->pipe;
+    for (int i = 0; i < fhe_ctx::Pipe::kSlots; ++i) {
+        if (P.st[i]) (void)hipStreamSynchronize(P.st[i]);
+        for (int j = 0; j < 3; ++j) {
+            if (P.pin[i][j]) (void)hipHostFree(P.pin[i][j]);
+            if (P.dev[i][j]) (void)hipFree(P.dev[i][j]);
+            P.pin[i][j] = P.dev[i][j] = nullptr;
+        }
+        if (P.done[i]) (void)hipEventDestroy(P.done[i]);
+        if (P.st[i]) (void)hipStreamDestroy(P.st[i]);
+        P.done[i] = nullptr;
+        P.st[i] = nullptr;
+    }
+    P.bytes = 0;
+}
+
 void free_tables(fhe_ctx *c) {
     void *p[5] = {c->tab.twf, c->tab.twi, c->tab.twist, c->tab.untwist, c->tab.untwist_r};
     for (void *x : p)
         if (x) (void)hipFree(x);
     c->tab = Tables{};
-    for (auto &s : c->scratch)
-        if (s) { (void)hipFree(s); s = nullptr; }
+    free_pipe(c);
     for (auto &s : c->plan.big_scratch)
         if (s) { (void)hipFree(s); s = nullptr; }
     if (c->br.exec) (void)hipGraphExecDestroy(c->br.exec);
@@ -316,39 +342,114 @@ int multi_one(fhe_ctx *m, int where, const void *probe, F &&fn) {
 #define FHE_MULTI_ONE(WHERE, PROBE, CALL) \
     if (c && c->multi()) return multi_one(c, (WHERE), (PROBE), [&](fhe_ctx *sub) { return [&](fhe_ctx *c) { return CALL; }(sub); })
 
-// Host staging: run fn(device pointers) over chunks of at most `chunk` polys.
-// nin inputs, one output; all of n*batch u64 per buffer (or `elems` each).
+// The context's plan with its launches redirected to stream s (the host
+// staging pipeline runs chunks on its own streams).
+static FHE_NS::Plan on(const fhe_ctx *c, hipStream_t s) {
+    FHE_NS::Plan p = c->plan;
+    p.stream = s;
+    return p;
+}
+
+#define FHE_TRY_STAGE(expr)                   \
+    do {                                      \
+        if (int _rc = (expr)) return _rc;     \
+    } while (0)
+
+// Host <-> pinned copy on several threads (a single thread moves ~10 GB/s
+// from pageable memory, well under what PCIe takes).
+static void par_copy(void *dst, const void *src, size_t bytes) {
+    static const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const size_t min_piece = (size_t)4 << 20;
+    const unsigned nt = (unsigned)std::max<size_t>(1, std::min<size_t>(hw, bytes / min_piece));
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t piece = (bytes / nt + 63) & ~(size_t)63;
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < nt; ++i) {
+        const size_t lo = i * piece;
+        if (lo >= bytes) break;
+        const size_t len = std::min(piece, bytes - lo);
+        th.emplace_back([=] { std::memcpy((char *)dst + lo, (const char *)src + lo, len); });
+    }
+    std::memcpy(dst, src, std::min(piece, bytes));
+    for (auto &t : th) t.join();
+}
+
+// Host staging: run fn(device pointers, n units, stream) over chunks of at
+// most FHE_STAGE_MB MiB per buffer (default 64), pipelined over the
+// context's kSlots slots (fhe_ctx::Pipe).  nin inputs, one output; all of
+// `*_elems_per_unit` u64 per unit.  Synchronous: returns once every output
+// chunk is back in `out`.
 template <typename F>
 int staged(fhe_ctx *c, const u64 *const *ins, int nin, size_t in_elems_per_unit, u64 *out,
            size_t out_elems_per_unit, size_t units, F &&fn) {
     std::lock_guard<std::mutex> lk(c->scratch_mu);
+    auto &P = c->pipe;
+    constexpr int S = fhe_ctx::Pipe::kSlots;
+    static const size_t stage_bytes = [] {
+        const char *v = std::getenv("FHE_STAGE_MB");
+        const size_t mb = v ? (size_t)std::strtoull(v, nullptr, 10) : 64;
+        return std::max<size_t>(1, mb) << 20;
+    }();
     const size_t max_unit_bytes = std::max(in_elems_per_unit, out_elems_per_unit) * sizeof(u64);
-    size_t chunk = std::max<size_t>(1, ((size_t)256 << 20) / max_unit_bytes);
+    size_t chunk = std::max<size_t>(1, stage_bytes / max_unit_bytes);
     chunk = std::min(chunk, units);
     const size_t need = chunk * max_unit_bytes;
-    if (c->scratch_bytes < need) {
-        for (auto &s : c->scratch)
-            if (s) { (void)hipFree(s); s = nullptr; }
-        c->scratch_bytes = 0;
-        for (auto &s : c->scratch) HIP_TRY(hipMalloc(&s, need), "hipMalloc(scratch)");
-        c->scratch_bytes = need;
+    if (P.bytes < need) {
+        free_pipe(c);
+        for (int i = 0; i < S; ++i) {
+            HIP_TRY(hipStreamCreateWithFlags(&P.st[i], hipStreamNonBlocking), "hipStreamCreate(stage)");
+            HIP_TRY(hipEventCreateWithFlags(&P.done[i], hipEventDisableTiming), "hipEventCreate(stage)");
+            for (int j = 0; j < 3; ++j) {
+                hipError_t e = hipMalloc(&P.dev[i][j], need);
+                if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMalloc(stage): out of memory");
+                HIP_TRY(e, "hipMalloc(stage)");
+                HIP_TRY(hipHostMalloc(&P.pin[i][j], need, hipHostMallocDefault), "hipHostMalloc(stage)");
+            }
+        }
+        P.bytes = need;
     }
-    for (size_t u0 = 0; u0 < units; u0 += chunk) {
-        const size_t nu = std::min(chunk, units - u0);
+    // order after work already queued on the context stream
+    hipEvent_t entry = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&entry, hipEventDisableTiming), "hipEventCreate");
+    HIP_TRY(hipEventRecord(entry, c->stream), "hipEventRecord");
+    for (int i = 0; i < S; ++i) HIP_TRY(hipStreamWaitEvent(P.st[i], entry, 0), "hipStreamWaitEvent");
+    (void)hipEventDestroy(entry);
+    const size_t nchunks = (units + chunk - 1) / chunk;
+    auto drain = [&](size_t k) -> int {  // chunk k's output back to `out`
+        const int sl = (int)(k % S);
+        HIP_TRY(hipEventSynchronize(P.done[sl]), "hipEventSynchronize(stage)");
+        const size_t u0 = k * chunk, nu = std::min(chunk, units - u0);
+        par_copy(out + u0 * out_elems_per_unit, P.pin[sl][2], nu * out_elems_per_unit * 8);
+        return FHE_OK;
+    };
+    int rc = FHE_OK;
+    for (size_t k = 0; k < nchunks && rc == FHE_OK; ++k) {
+        const int sl = (int)(k % S);
+        if (k >= (size_t)S && (rc = drain(k - S)) != FHE_OK) break;
+        const size_t u0 = k * chunk, nu = std::min(chunk, units - u0);
         const u64 *dins[3] = {nullptr, nullptr, nullptr};
         for (int i = 0; i < nin; ++i) {
-            HIP_TRY(hipMemcpyAsync(c->scratch[i], ins[i] + u0 * in_elems_per_unit, nu * in_elems_per_unit * 8,
-                                   hipMemcpyHostToDevice, c->stream),
-                    "hipMemcpyAsync(H2D)");
-            dins[i] = (const u64 *)c->scratch[i];
+            const size_t b = nu * in_elems_per_unit * 8;
+            par_copy(P.pin[sl][i], ins[i] + u0 * in_elems_per_unit, b);
+            hipError_t e = hipMemcpyAsync(P.dev[sl][i], P.pin[sl][i], b, hipMemcpyHostToDevice, P.st[sl]);
+            if (e != hipSuccess) { rc = hip_fail(e, "hipMemcpyAsync(H2D)"); break; }
+            dins[i] = (const u64 *)P.dev[sl][i];
         }
-        u64 *dout = (u64 *)c->scratch[2];
-        HIP_TRY(fn(dins, dout, nu), "kernel launch");
-        HIP_TRY(hipMemcpyAsync(out + u0 * out_elems_per_unit, dout, nu * out_elems_per_unit * 8,
-                               hipMemcpyDeviceToHost, c->stream),
-                "hipMemcpyAsync(D2H)");
-        HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+        if (rc != FHE_OK) break;
+        hipError_t e = fn(dins, (u64 *)P.dev[sl][2], nu, P.st[sl]);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(P.pin[sl][2], P.dev[sl][2], nu * out_elems_per_unit * 8, hipMemcpyDeviceToHost, P.st[sl]);
+        if (e == hipSuccess) e = hipEventRecord(P.done[sl], P.st[sl]);
+        if (e != hipSuccess) rc = hip_fail(e, "kernel launch");
     }
+    if (rc != FHE_OK) {
+        for (int i = 0; i < S; ++i) (void)hipStreamSynchronize(P.st[i]);
+        return rc;
+    }
+    for (size_t k = nchunks > (size_t)S ? nchunks - S : 0; k < nchunks; ++k) FHE_TRY_STAGE(drain(k));
     return FHE_OK;
 }
 
@@ -363,7 +464,7 @@ int run_poly_op(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, size_t batch, 
     DeviceGuard g(c->device);
     if (where == FHE_DEVICE) {
         const u64 *ins[3] = {a, b, nullptr};
-        HIP_TRY(fn(ins, out, batch), "kernel launch");
+        HIP_TRY(fn(ins, out, batch, c->stream), "kernel launch");
         return FHE_OK;
     }
     const u64 *ins[2] = {a, b};
@@ -677,28 +778,28 @@ int fhe_ntt_fwd_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batc
     FHE_MULTI(batch, where, in, fhe_ntt_fwd_batch(c, in + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 0); });
+                       [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) { return FHE_NS::launch_fwd(on(c, st), d[0], o, nb, 0); });
 }
 int fhe_ntt_inv_batch(fhe_ctx *c, const uint64_t *in, uint64_t *out, size_t batch, int where) {
     FHE_MULTI(batch, where, in, fhe_ntt_inv_batch(c, in + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     return run_poly_op(c, in, nullptr, out, batch, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_inv(c->plan, d[0], o, nb); });
+                       [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) { return FHE_NS::launch_inv(on(c, st), d[0], o, nb); });
 }
 int fhe_ntt_fwd_mul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch, int where) {
     FHE_MULTI(batch, where, a, fhe_ntt_fwd_mul_batch(c, a + lo * c->n, w + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!w && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
-    return run_poly_op(c, a, w, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_fwd_mul(c->plan, d[0], d[1], o, nb);
+    return run_poly_op(c, a, w, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_fwd_mul(on(c, st), d[0], d[1], o, nb);
     });
 }
 int fhe_polymul_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
     FHE_MULTI(batch, where, a, fhe_polymul_batch(c, a + lo * c->n, b + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
-    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_polymul(c->plan, d[0], d[1], o, nb);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_polymul(on(c, st), d[0], d[1], o, nb);
     });
 }
 int fhe_pointwise_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
@@ -706,8 +807,8 @@ int fhe_pointwise_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const FHE_NS::ModConsts m = mod_consts(c->q);
-    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_modmul(m, d[0], d[1], o, nb * c->n, c->stream);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_modmul(m, d[0], d[1], o, nb * c->n, st);
     });
 }
 int fhe_poly_add_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
@@ -715,8 +816,8 @@ int fhe_poly_add_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const FHE_NS::ModConsts m = mod_consts(c->q);
-    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_addsub(m, d[0], d[1], o, nb * c->n, 0, c->stream);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_addsub(m, d[0], d[1], o, nb * c->n, 0, st);
     });
 }
 int fhe_poly_sub_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t batch, int where) {
@@ -724,15 +825,15 @@ int fhe_poly_sub_batch(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_
     if (int rc = check_ctx(c)) return rc;
     if (!b && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const FHE_NS::ModConsts m = mod_consts(c->q);
-    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_addsub(m, d[0], d[1], o, nb * c->n, 1, c->stream);
+    return run_poly_op(c, a, b, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_addsub(m, d[0], d[1], o, nb * c->n, 1, st);
     });
 }
 int fhe_poly_neg_batch(fhe_ctx *c, const uint64_t *a, uint64_t *out, size_t batch, int where) {
     FHE_MULTI(batch, where, a, fhe_poly_neg_batch(c, a + lo * c->n, out + lo * c->n, nb, where));
     if (int rc = check_ctx(c)) return rc;
-    return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_neg(c->q, d[0], o, nb * c->n, c->stream);
+    return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_neg(c->q, d[0], o, nb * c->n, st);
     });
 }
 int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, uint64_t *out, size_t batch,
@@ -742,8 +843,8 @@ int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, ui
     const FHE_NS::ModConsts m = mod_consts(c->q);
     const u64 s = scalar % c->q;
     const u64 sp = (u64)(((u128)s << 64) / c->q);
-    return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_mul_scalar(m, d[0], s, sp, o, nb * c->n, c->stream);
+    return run_poly_op(c, a, nullptr, out, batch, where, c->n, c->n, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_mul_scalar(m, d[0], s, sp, o, nb * c->n, st);
     });
 }
 
@@ -765,7 +866,7 @@ int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggs
     if (level == 0) return fail(FHE_ERR_INVALID_ARG, "level must be >= 1");
     const size_t polys = (size_t)(k + 1) * level * (k + 1);
     return run_poly_op(c, ggsw, nullptr, ggsw_ntt, polys, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 1); });
+                       [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) { return FHE_NS::launch_fwd(on(c, st), d[0], o, nb, 1); });
 }
 
 int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
@@ -784,14 +885,14 @@ int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32
         hipError_t e = hipMemcpy(dk, ggsw_ntt, kbytes, hipMemcpyHostToDevice);
         int rc = e != hipSuccess ? hip_fail(e, "hipMemcpy(ggsw)") : FHE_OK;
         if (rc == FHE_OK)
-            rc = run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb) {
-                return FHE_NS::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], (const u64 *)dk, o, nb);
+            rc = run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+                return FHE_NS::launch_extprod(on(c, st), (int)k + 1, (int)level, (int)base_log, d[0], (const u64 *)dk, o, nb);
             });
         (void)hipFree(dk);
         return rc;
     }
-    return run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb) {
-        return FHE_NS::launch_extprod(c->plan, (int)k + 1, (int)level, (int)base_log, d[0], ggsw_ntt, o, nb);
+    return run_poly_op(c, glwe, nullptr, out, batch, where, per, per, [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+        return FHE_NS::launch_extprod(on(c, st), (int)k + 1, (int)level, (int)base_log, d[0], ggsw_ntt, o, nb);
     });
 }
 
@@ -803,8 +904,8 @@ int fhe_decompose_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uin
         return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
     const FHE_NS::ModConsts m = mod_consts(c->q);
     return run_poly_op(c, poly, nullptr, out, npoly, where, c->n, (size_t)c->n * level,
-                       [&](const u64 *const *d, u64 *o, size_t nb) {
-                           return FHE_NS::launch_decompose(m, d[0], o, c->n, nb, base_log, level, c->stream);
+                       [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) {
+                           return FHE_NS::launch_decompose(m, d[0], o, c->n, nb, base_log, level, st);
                        });
 }
 
@@ -830,7 +931,7 @@ int fhe_relin_key_prepare(fhe_ctx *c, uint32_t level, const uint64_t *rlk, uint6
     if (int rc = check_ctx(c)) return rc;
     FHE_TRY(check_fused(c, "relinearisation"));
     return run_poly_op(c, rlk, nullptr, rlk_ntt, (size_t)2 * level, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 1); });
+                       [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) { return FHE_NS::launch_fwd(on(c, st), d[0], o, nb, 1); });
 }
 
 int fhe_relinearize_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *ct3,
@@ -929,7 +1030,7 @@ int fhe_public_key_prepare(fhe_ctx *c, const uint64_t *pk, uint64_t *pk_prep, in
     if (int rc = check_ctx(c)) return rc;
     FHE_TRY(check_fused(c, "encryption"));
     return run_poly_op(c, pk, nullptr, pk_prep, 2, where, c->n, c->n,
-                       [&](const u64 *const *d, u64 *o, size_t nb) { return FHE_NS::launch_fwd(c->plan, d[0], o, nb, 1); });
+                       [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) { return FHE_NS::launch_fwd(on(c, st), d[0], o, nb, 1); });
 }
 
 int fhe_encrypt_batch(fhe_ctx *c, uint64_t t, const uint64_t *pk_prep, const uint64_t *values, const uint64_t *u,
