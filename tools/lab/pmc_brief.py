@@ -13,4 +13,4 @@ for f in sys.argv[1:]:
     print(f, f"{ns / 1e6:.3f} ms vgpr {s.get('vgpr')} clk {clk:.2f} GHz")
     print("  per wave:", {k[3:]: round(v / p["SQ_WAVES"]) for k, v in p.items() if k.startswith("SQ_") and k != "SQ_WAVES"})
     print(f"  wait_any {p['SQ_WAIT_ANY'] / w:.2f} wait_inst {p['SQ_WAIT_INST_ANY'] / w:.2f} "
-          f"active {p['SQ_ACTIVE_INST_ANY'] / w:.2f} lds_conflict/lds_active {p['SQ_LDS_BANK_CONFLICT'] / max(1, p['SQ_LDS_IDX_ACTIVE']):.2f}")
+          f"active {p['SQ_ACTIVE_INST_ANY'] / w:.2f} lds_conflict/lds_active {p['SQ_LDS_BANK_CONFLICT'] / max(1, p.get('SQ_LDS_IDX_ACTIVE', 0)):.2f}")
