@@ -76,7 +76,7 @@ k_big_inv_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size
     const auto r = brsrc(in + (poly << (kBigS + M)) + ((size_t)b << kBigS));
     const uint32_t vo = LastIO<kBigS>::vo(tau);
     W v[G::E];
-    load_coeffs<G::E>(v, (uint64_t)A.ar.q2, A.q64, A.mu64,
+    load_coeffs_r<G::E>(v, (uint64_t)A.ar.q2, SlowRed<W>{A},
                       [&](int e) -> uint64_t { return bload(r, vo, LastIO<kBigS>::so(e)); });
     inv_poly_from_regs<kBigS, NEGA>(lds, v, tau, out + (poly << (kBigS + M)) + o, valid, A,
                                     MONT ? A.ninv_r : A.ninv, MONT ? A.untwist_r : A.untwist, M, o);

@@ -183,6 +183,69 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow + 2 * G::N, valid, A, A.ninv_r, A.untwist_r);
 }
 
+// 32 coefficients per thread (q < 2^30, N = 8192 / 16384): two workgroups
+// per CU, every transform pair in lockstep (fwd_poly2 / inv_poly2):
+//   1. X0, Y0 = fwd(x0), fwd(y0)          stash canon(X0), canon(Y0) as W words
+//                                          in rows 1 / 2 of the output (own
+//                                          positions, overwritten last)
+//   2. c0 = inv(X0 Y0)                     -> row 0
+//   3. X1, Y1 = fwd(x1), fwd(y1)
+//   4. c1 = X0 Y1 + X1 Y0, c2 = X1 Y1      (X0, Y0 back from the stash)
+//   5. inv(c1), inv(c2)                    -> rows 1, 2
+// 72 B per coefficient of HBM traffic (56 + the 16 B stash round trip) for
+// two-workgroup occupancy and shared twiddles; FHE_CTMUL_E16=1 keeps the
+// 16-per-thread kernel (lab A/B).
+#ifndef FHE_CTMUL_E16
+#define FHE_CTMUL_E16 0
+#endif
+template <int LOGN, typename W, bool NEGA, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *out, size_t batch,
+          NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    static_assert(G::P == 1 && G::LOGE == 5, "one ciphertext pair per workgroup, 32 coefficients per thread");
+    constexpr int PF = 1;
+    __shared__ W lds[G::LW];
+    const uint32_t tau = threadIdx.x;
+    const size_t poly = blockIdx.x;
+    if (poly >= batch) return;
+    const uint64_t *xr = x + poly * 2 * G::N, *yr = y + poly * 2 * G::N;
+    uint64_t *orow = out + poly * 3 * G::N;
+    W *s1 = reinterpret_cast<W *>(orow + G::N), *s2 = reinterpret_cast<W *>(orow + 2 * G::N);
+    W a[G::E], b[G::E];
+    // 1-2
+    fwd_poly2<LOGN, NEGA, LAZY, PF>(lds, a, b, tau, xr, yr, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
+        const W x0 = fwd_to_canon<LAZY>(a[e], A);
+        s1[gi] = x0;
+        s2[gi] = fwd_to_canon<LAZY>(b[e], A);
+        a[e] = A.ar.mont(x0, b[e]);
+    }
+    __syncthreads();
+    uint32_t t1 = tau;
+    asm volatile("" : "+v"(t1));
+    inv_poly_from_regs<LOGN, NEGA, PF>(lds, a, t1, orow, true, A, A.ninv_r, A.untwist_r);
+    __syncthreads();
+    // 3-4
+    uint32_t t2 = tau;
+    asm volatile("" : "+v"(t2));
+    fwd_poly2<LOGN, NEGA, LAZY, PF>(lds, a, b, t2, xr + G::N, yr + G::N, A);
+#pragma unroll
+    for (int e = 0; e < G::E; ++e) {
+        const uint32_t gi = gidx<LOGN, G::NP - 1>(t2, e);
+        const W x1 = fwd_to_canon<LAZY>(a[e], A);
+        const W c1 = A.ar.red2q(A.ar.mont(s1[gi], b[e]) + A.ar.mont(x1, s2[gi]));
+        b[e] = A.ar.mont(x1, b[e]);
+        a[e] = c1;
+    }
+    __syncthreads();  // every stash read precedes the final stores of rows 1 / 2
+    uint32_t t3 = tau;
+    asm volatile("" : "+v"(t3));
+    inv_poly2<LOGN, NEGA, PF>(lds, a, b, t3, orow + G::N, orow + 2 * G::N, A, A.ninv_r, A.untwist_r);
+}
+
 template <int LOGN, typename W, bool NEGA>
 static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *x, const uint64_t *y, uint64_t *out,
                             size_t batch) {
@@ -190,6 +253,16 @@ static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *
     const size_t blocks = (batch + G::P - 1) / G::P;
     bool lazy = false;
     if constexpr (sizeof(W) == 4) lazy = p.lazy;
+    if constexpr (sizeof(W) == 4 && (LOGN == 13 || LOGN == 14) && !FHE_CTMUL_E16) {
+        constexpr int K = gk(LOGN, 5);
+        if (lazy)
+            hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, true>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y, out,
+                               batch, A);
+        else
+            hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, false>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y,
+                               out, batch, A);
+        return hipGetLastError();
+    }
     if (lazy) {
         if constexpr (sizeof(W) == 4)
             hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,

@@ -498,44 +498,77 @@ __device__ __forceinline__ W fwd_to_canon(W x, const NttArgs<W> &A) {
     return A.ar.red1q(fwd_to_2q<LAZY>(x, A));
 }
 
+// Exact reduction of an out-of-range input word (any u64 behaves as x mod q).
+// 32-bit lanes: x = hi 2^32 + lo -> shoup(hi, 2^32 mod q) + shoup(lo, 1),
+// then canonical -- 32-bit multiplies only, a few registers (the 64-bit
+// Barrett step of mod64_slow spilled in the cold paths of the 32-coefficient
+// kernels).  64-bit lanes: mod64_slow.
+template <typename W>
+struct SlowRed {
+    const NttArgs<W> &A;
+    __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
+        if constexpr (sizeof(W) == 4) {
+            const W r = A.ar.shoup((W)(x >> 32), A.rmod) + A.ar.shoup((W)x, A.one);  // [0, 4q)
+            return (uint64_t)A.ar.canon4(r);
+        } else {
+            return mod64_slow(x, A.q64, A.mu64);
+        }
+    }
+};
+struct Mod64Red {
+    uint64_t q, mu;
+    __device__ __forceinline__ uint64_t operator()(uint64_t x) const { return mod64_slow(x, q, mu); }
+};
+
 // E coefficients of one polynomial from HBM into the lazy range [0, lim) of
-// word W.  Out-of-range inputs (any u64 behaves as x mod q) take one
-// divergent slow path for the whole thread.
-template <int E, typename W>
-__device__ __forceinline__ void coeffs_from_raw(W (&v)[E], uint64_t (&raw)[E], uint64_t lim, uint64_t q, uint64_t mu) {
+// word W.  Out-of-range inputs take one divergent slow path for the whole
+// thread, one element at a time (a scheduling barrier each: no spills).
+template <int E, typename W, typename RD>
+__device__ __forceinline__ void coeffs_from_raw(W (&v)[E], uint64_t (&raw)[E], uint64_t lim, RD &&red) {
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < E; ++t) bad |= raw[t] >= lim;
     if (__builtin_expect(bad, 0)) {
 #pragma unroll
-        for (int t = 0; t < E; ++t)
-            {
-                if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
-                __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time (no spills)
-            }
+        for (int t = 0; t < E; ++t) {
+            if (raw[t] >= lim) raw[t] = red(raw[t]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
 #pragma unroll
     for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
 }
+template <int E, typename W>
+__device__ __forceinline__ void coeffs_from_raw(W (&v)[E], uint64_t (&raw)[E], uint64_t lim, uint64_t q, uint64_t mu) {
+    coeffs_from_raw<E>(v, raw, lim, Mod64Red{q, mu});
+}
+// The raw words are narrowed as soon as they are checked; an out-of-range
+// word is loaded again in the (cold) slow path, so no 64-bit word stays live
+// across it (that is what spilled).
+template <int E, typename W, typename RD, typename F>
+__device__ __forceinline__ void load_coeffs_r(W (&v)[E], uint64_t lim, RD &&red, F &&addr_of) {
+    uint64_t raw[E];
+#pragma unroll
+    for (int t = 0; t < E; ++t) raw[t] = addr_of(t);
+    uint32_t bad = 0;
+#pragma unroll
+    for (int t = 0; t < E; ++t) {
+        bad |= uint32_t(raw[t] >= lim) << t;
+        v[t] = W(raw[t]);
+    }
+    if (__builtin_expect(bad != 0, 0)) {
+#pragma unroll
+        for (int t = 0; t < E; ++t)
+            if ((bad >> t) & 1) v[t] = W(red(addr_of(t)));
+    }
+}
+// Computed digit loads (k_dmac): no reload (the lambda is not a plain load).
 template <int E, typename W, typename F>
 __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q, uint64_t mu, F &&addr_of) {
     uint64_t raw[E];
-    bool bad = false;
 #pragma unroll
-    for (int t = 0; t < E; ++t) {
-        raw[t] = addr_of(t);
-        bad |= raw[t] >= lim;
-    }
-    if (__builtin_expect(bad, 0)) {
-#pragma unroll
-        for (int t = 0; t < E; ++t)
-            {
-                if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
-                __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time (no spills)
-            }
-    }
-#pragma unroll
-    for (int t = 0; t < E; ++t) v[t] = W(raw[t]);
+    for (int t = 0; t < E; ++t) raw[t] = addr_of(t);
+    coeffs_from_raw<E>(v, raw, lim, Mod64Red{q, mu});
 }
 
 #ifndef FHE_LOAD_INFLIGHT
@@ -545,8 +578,10 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
 // each, so only IN chunks of CH are in flight at once and each chunk is
 // narrowed before the next is issued (scheduling barriers keep the compiler
 // from hoisting all 32 loads, which spills beside a parked spectrum).
-template <int E, int CH, int IN, typename W, typename F>
-__device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, uint64_t q, uint64_t mu, F &&addr_of) {
+// RELOAD = false keeps each chunk's raw words live through the slow path
+// instead (measured: fewer spills when a pre-twist follows the load).
+template <int E, int CH, int IN, bool RELOAD = true, typename W, typename RD, typename F>
+__device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, RD &&red, F &&addr_of) {
     constexpr int NC = E / CH;
     uint64_t raw[E];
 #pragma unroll
@@ -560,19 +595,32 @@ __device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, uin
             for (int t = (c + IN) * CH; t < (c + IN) * CH + CH; ++t) raw[t] = addr_of(t);
         }
         __builtin_amdgcn_sched_barrier(0);
-        bool bad = false;
+        if constexpr (RELOAD) {
+            uint32_t bad = 0;
 #pragma unroll
-        for (int t = c * CH; t < c * CH + CH; ++t) bad |= raw[t] >= lim;
-        if (__builtin_expect(bad, 0)) {
-#pragma unroll
-            for (int t = c * CH; t < c * CH + CH; ++t)
-                {
-                if (raw[t] >= lim) raw[t] = mod64_slow(raw[t], q, mu);
-                __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time (no spills)
+            for (int t = c * CH; t < c * CH + CH; ++t) {
+                bad |= uint32_t(raw[t] >= lim) << (t - c * CH);
+                v[t] = W(raw[t]);
             }
-        }
+            if (__builtin_expect(bad != 0, 0)) {  // reload and reduce (see load_coeffs_r)
 #pragma unroll
-        for (int t = c * CH; t < c * CH + CH; ++t) v[t] = W(raw[t]);
+                for (int t = c * CH; t < c * CH + CH; ++t)
+                    if ((bad >> (t - c * CH)) & 1) v[t] = W(red(addr_of(t)));
+            }
+        } else {
+            bool bad = false;
+#pragma unroll
+            for (int t = c * CH; t < c * CH + CH; ++t) bad |= raw[t] >= lim;
+            if (__builtin_expect(bad, 0)) {
+#pragma unroll
+                for (int t = c * CH; t < c * CH + CH; ++t) {
+                    if (raw[t] >= lim) raw[t] = red(raw[t]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int t = c * CH; t < c * CH + CH; ++t) v[t] = W(raw[t]);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -606,15 +654,15 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
     // Shoup-based first steps (twist / R-scaling) accept any word
     const uint64_t lim = (NEGA || RS) ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     if (pre) {  // prefetched by the caller (load_raw)
-        coeffs_from_raw<G::E>(v, *pre, lim, A.q64, A.mu64);
+        coeffs_from_raw<G::E>(v, *pre, lim, SlowRed<W>{A});
     } else if constexpr (G::P == 1) {  // the caller has returned early if !valid
         const auto r = brsrc(src);
         const uint32_t vo = (tau << sh) * 8u;
         auto at = [&](int t) -> uint64_t { return bload(r, vo, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u); };
-        if constexpr (G::LOGE == 5) load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, A.q64, A.mu64, at);
-        else load_coeffs<G::E>(v, lim, A.q64, A.mu64, at);
+        if constexpr (G::LOGE == 5) load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT, !NEGA>(v, lim, SlowRed<W>{A}, at);
+        else load_coeffs_r<G::E>(v, lim, SlowRed<W>{A}, at);
     } else {
-        load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+        load_coeffs_r<G::E>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return valid ? __builtin_nontemporal_load(src + ((tau + cbrv(t, G::LOGE) * G::T) << sh)) : 0;
         });
     }
@@ -641,13 +689,13 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     const uint32_t vo = tau * 8u;
     {
         const auto r = brsrc(src);
-        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT, !NEGA>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
         });
     }
     {
         const auto r = brsrc(src2);
-        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v2, lim, A.q64, A.mu64, [&](int t) -> uint64_t {
+        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT, !NEGA>(v2, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
         });
     }
@@ -699,6 +747,70 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
             bstore(brsrc(dst), (tau << sh) * 8u, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u, y);
         else if (valid)
             __builtin_nontemporal_store(y, dst + gi);
+    }
+}
+
+// Two inverse transforms in lockstep (shared twiddles, two butterfly
+// streams), every pass staged (the last pass too: two 32-word spectra leave
+// no room for a whole pass of twiddles).  Inputs in [0, 2q), last-pass
+// layout; canonical outputs stored to dst / dst2 (P == 1).
+template <int LOGN, int PASS, int K, int LOOK, bool FOLD, typename W>
+__device__ __forceinline__ void inv_stages2(uint32_t tau, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E],
+                                            Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT], const Tw<W> *__restrict__ tw,
+                                            const Arith<W> &ar, Tw<W> scale) {
+    if constexpr (K >= 0) {
+        if constexpr (K - LOOK >= 0) load_tw<LOGN, PASS, W, K - LOOK, K - LOOK + 1>(tau, tw, t);
+        inv_stage<LOGN, PASS, K, FOLD>(v, t, ar, scale);
+        inv_stage<LOGN, PASS, K, FOLD>(v2, t, ar, scale);
+        __builtin_amdgcn_sched_barrier(0);
+        inv_stages2<LOGN, PASS, K - 1, LOOK, FOLD>(tau, v, v2, t, tw, ar, scale);
+    }
+}
+template <int LOGN, int PASS, bool FOLD, int PF, typename W>
+__device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
+                                          const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale) {
+    if constexpr (PASS >= 0) {
+        Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        constexpr int R = PassTw<LOGN, PASS>::R;
+        constexpr int KS = R - PF < 0 ? 0 : R - PF;
+        load_tw<LOGN, PASS, W, KS, 8>(tau, tw, t);
+        lds_store<LOGN, PASS + 1>(lds, v, tau);
+        __syncthreads();
+        lds_load<LOGN, PASS>(lds, v, tau);
+        __syncthreads();
+        lds_store<LOGN, PASS + 1>(lds, v2, tau);
+        __syncthreads();
+        lds_load<LOGN, PASS>(lds, v2, tau);
+        inv_stages2<LOGN, PASS, R - 1, R - KS, FOLD>(tau, v, v2, t, tw, ar, scale);
+        inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);
+    }
+}
+template <int LOGN, bool NEGA, int PF, typename W>
+__device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
+                                          uint64_t *__restrict__ dst, uint64_t *__restrict__ dst2,
+                                          const NttArgs<W> &A, Tw<W> scale, const Tw<W> *__restrict__ post) {
+    using G = Geo<LOGN>;
+    static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
+    constexpr int LAST = G::NP - 1;
+    {
+        Tw<W> t[PassTw<LOGN, LAST>::COUNT];
+        constexpr int R = PassTw<LOGN, LAST>::R;
+        constexpr int KS = R - PF < 0 ? 0 : R - PF;
+        load_tw<LOGN, LAST, W, KS, 8>(tau, A.twi, t);
+        inv_stages2<LOGN, LAST, R - 1, R - KS, !NEGA>(tau, v, v2, t, A.twi, A.ar, scale);
+    }
+    inv_rest2<LOGN, LAST - 1, !NEGA, PF>(lds, v, v2, tau, A.twi, A.ar, scale);
+    const auto r1 = brsrc(dst), r2 = brsrc(dst2);
+#pragma unroll
+    for (int t = 0; t < G::E; ++t) {
+        const uint32_t gi = tau + cbrv(t, G::LOGE) * G::T;
+        W x = v[t], x2 = v2[t];
+        if constexpr (NEGA) {
+            x = A.ar.shoup(x, post[gi]);
+            x2 = A.ar.shoup(x2, post[gi]);
+        }
+        bstore(r1, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, (uint64_t)A.ar.red1q(x));
+        bstore(r2, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, (uint64_t)A.ar.red1q(x2));
     }
 }
 

@@ -67,7 +67,7 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
         };
         fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A, 0, 0, hook);
         W w[G::E];
-        coeffs_from_raw<G::E>(w, rw, A.q64, A.q64, A.mu64);
+        coeffs_from_raw<G::E>(w, rw, A.q64, SlowRed<W>{A});
         const auto ro = brsrc(dst);
 #pragma unroll
         for (int e = 0; e < G::E; ++e) bstore(ro, vo, LastIO<LOGN>::so(e), (uint64_t)A.ar.red1q(A.ar.mont(v[e], w[e])));
@@ -84,13 +84,13 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
         if constexpr (G::P == 1) {
             const auto rw = brsrc(wp), ro = brsrc(dst);
             const uint32_t vo = LastIO<LOGN>::vo(tau);
-            load_coeffs<CH>(w, A.q64, A.q64, A.mu64,
+            load_coeffs_r<CH>(w, A.q64, SlowRed<W>{A},
                             [&](int e) -> uint64_t { return bload(rw, vo, LastIO<LOGN>::so(c0 + e)); });
 #pragma unroll
             for (int e = 0; e < CH; ++e)
                 bstore(ro, vo, LastIO<LOGN>::so(c0 + e), (uint64_t)A.ar.red1q(A.ar.mont(v[c0 + e], w[e])));
         } else {
-            load_coeffs<CH>(w, A.q64, A.q64, A.mu64, [&](int e) -> uint64_t {
+            load_coeffs_r<CH>(w, A.q64, SlowRed<W>{A}, [&](int e) -> uint64_t {
                 return __builtin_nontemporal_load(wp + gidx<LOGN, G::NP - 1>(tau, c0 + e));
             });
 #pragma unroll

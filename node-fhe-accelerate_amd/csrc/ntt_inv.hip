@@ -24,7 +24,7 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     if constexpr (G::P == 1) {
         const auto r = brsrc(src);
         const uint32_t vo = LastIO<LOGN>::vo(tau);
-        load_coeffs<G::E>(v, lim, A.q64, A.mu64, [&](int e) -> uint64_t { return bload(r, vo, LastIO<LOGN>::so(e)); });
+        load_coeffs_r<G::E>(v, lim, SlowRed<W>{A}, [&](int e) -> uint64_t { return bload(r, vo, LastIO<LOGN>::so(e)); });
     } else {
 #pragma unroll
         for (int e = 0; e < G::E; ++e) {
