@@ -166,3 +166,41 @@ def test_parameter_presets():
     ckks = P.gpu_moduli(P.create_parameter_set("ckks-128-ml"))
     assert [m["usable"] for m in ckks] == [True, False, False, False, False]  # only Q_60_1 admits N = 16384
     assert all(m["usable"] for m in P.gpu_moduli(P.create_parameter_set("bfv-128-simd")))
+
+
+# ------------------------------------------------------------ register budget
+# Kernels of the measured paths must run without scratch:
+# the BASELINE workloads (C3 fwd+modmul, C4 polymul, both primes), the
+# transforms, the external product and the single-launch blind rotation.
+SCRATCH_FREE = [
+    "k_ntt_fwd_mul<14, unsigned int, false, true>", "k_ntt_fwd_mul<14, unsigned long, false, false>",
+    "k_polymul2<1294, unsigned int, false, true>", "k_polymul<14, unsigned long, false, false>",
+    "k_ntt_fwd<14, unsigned int, false, true, 0>", "k_ntt_fwd<14, unsigned long, false, false, 0>",
+    "k_ntt_inv<14, unsigned int, false>", "k_ntt_inv<14, unsigned long, false>",
+    "k_dmac<14, unsigned long, false, 2, false, 0>", "k_br_persist<",
+]
+# Ratchet: kernels that still use scratch anywhere (mostly the cold
+# out-of-range-input paths of small-degree and negacyclic instantiations);
+# the count may only go down.
+SCRATCH_CEILING = 93
+
+
+def test_kernel_scratch_budget():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as kr
+
+    import glob
+
+    if not glob.glob(os.path.join(kr.OBJ_DIR, "*.o")):
+        pytest.skip("objects not built (run __graft_entry__.build())")
+    ks = kr.kernels()
+    names = kr.demangle([k["name"] for k in ks])
+    for pat in SCRATCH_FREE:
+        hits = [(n, k) for n, k in zip(names, ks) if pat in n]
+        assert hits, f"no kernel matches {pat}"
+        for n, k in hits:
+            assert k["scratch"] == 0 and k["vgpr_spill"] == 0, (n, k["scratch"], k["vgpr_spill"])
+    with_scratch = [n for n, k in zip(names, ks) if k["scratch"]]
+    assert len(with_scratch) <= SCRATCH_CEILING, with_scratch
