@@ -21,7 +21,22 @@
 namespace FHE_NS {
 
 __device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
-__device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
+// 64 x 64 -> high 64.  FHE_MULHI64=1: the middle partial products summed with
+// a 65-bit carry (two full-width mads) instead of two zero-extended halves
+// (the compiler builds those pairs with 3 v_mov per product).
+#ifndef FHE_MULHI64
+#define FHE_MULHI64 0
+#endif
+__device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
+#if FHE_MULHI64
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t m1 = (uint64_t)a1 * b0 + __umulhi(a0, b0);             // < 2^64
+    const unsigned __int128 m2 = (unsigned __int128)((uint64_t)a0 * b1) + m1;  // < 2^65
+    return (uint64_t)a1 * b1 + (uint64_t)(m2 >> 32);
+#else
+    return __umul64hi(a, b);
+#endif
+}
 // unsigned min: x - k wraps above x when x < k, so min() keeps x.
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return a < b ? a : b; }

@@ -234,11 +234,88 @@ k_dmac(DmArgs D, NttArgs<W> A) {
     }
 }
 
+// External product with one decomposition level (level == 1, K1 == 2) for
+// one polynomial per workgroup: the two digit polynomials are transformed in
+// lockstep (shared twiddles), the key MAC turns (X0, X1) into the two
+// NTT-domain outputs in place, and both inverses run in lockstep -- nothing
+// is parked in HBM (k_dmac's output-row stash read and wrote every
+// accumulator once per row: 2.2x the algorithmic traffic at N = 16384).
+#ifndef FHE_EXT2_PF
+#define FHE_EXT2_PF 0
+#endif
+#ifndef FHE_EXT2
+#define FHE_EXT2 1
+#endif
+template <int LOGN, typename W, bool NEGA>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_extprod2(DmArgs D, NttArgs<W> A) {
+    using G = Geo<LOGN>;
+    static_assert(G::P == 1, "one ciphertext per workgroup");
+    constexpr int PF = FHE_EXT2_PF;
+    __shared__ W lds[G::LW];
+    const uint32_t tau = threadIdx.x;
+    const size_t poly = blockIdx.x;
+    if (poly >= D.batch) return;
+    const uint64_t *srow = D.src + poly * 2 * G::N;
+    uint64_t *orow = D.out + poly * 2 * G::N;
+    const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    const uint64_t q = A.q64, mu = A.mu64, lim = (uint64_t)A.ar.q2 * 2;
+    W v0[G::E], v1[G::E];
+    Tw<W> t0[PassTw<LOGN, 0>::COUNT];
+    load_tw<LOGN, 0>(tau, A.twf, t0);
+    // digit (level 0 of 1: shift 0) of glwe row i, signed (decompose_polynomial)
+    auto digit = [&](const uint64_t *src, int t) -> uint64_t {
+        uint64_t d = src[tau + cbrv(t, G::LOGE) * G::T] & mask;
+        if (d > half) d = red_q(q - (base - d), q, mu);
+        return d;
+    };
+    load_coeffs<G::E>(v0, lim, q, mu, [&](int t) { return digit(srow, t); });
+    load_coeffs<G::E>(v1, lim, q, mu, [&](int t) { return digit(srow + G::N, t); });
+    if constexpr (NEGA) {
+#pragma unroll
+        for (int t = 0; t < G::E; ++t) {
+            const Tw<W> tw = A.twist[tau + cbrv(t, G::LOGE) * G::T];
+            v0[t] = A.ar.shoup(v0[t], tw);
+            v1[t] = A.ar.shoup(v1[t], tw);
+        }
+    }
+    fwd_pass<LOGN, 0, false>(v0, t0, A.ar);
+    fwd_pass<LOGN, 0, false>(v1, t0, A.ar);
+    fwd_rest2<LOGN, 1, false, PF>(lds, v0, v1, tau, A.twf, A.ar);
+    // (o0, o1) = (X0 G00 + X1 G10, X0 G01 + X1 G11); raw outputs (< 4q) times
+    // canonical prepared keys: valid Montgomery pairs
+    const uint64_t *g = D.key;
+#pragma unroll
+    for (int e0 = 0; e0 < G::E; e0 += 2) {
+        uint64_t k[2][4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) k[e][j] = g[(size_t)j * G::N + gidx<LOGN, G::NP - 1>(tau, e0 + e)];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const W x0 = v0[e0 + e], x1 = v1[e0 + e];
+            v0[e0 + e] = A.ar.red2q(A.ar.mont(x0, (W)k[e][0]) + A.ar.mont(x1, (W)k[e][2]));
+            v1[e0 + e] = A.ar.red2q(A.ar.mont(x0, (W)k[e][1]) + A.ar.mont(x1, (W)k[e][3]));
+        }
+    }
+    __syncthreads();
+    uint32_t ti = tau;
+    asm volatile("" : "+v"(ti));
+    inv_poly2<LOGN, NEGA, PF>(lds, v0, v1, ti, orow, orow + G::N, A, A.ninv, A.untwist);
+}
+
 template <int LOGN, typename W, bool NEGA, int MODE>
 static hipError_t dmac_one(const NttArgs<W> &A, hipStream_t s, int k1, const DmArgs &D) {
     using G = Geo<LOGN>;
     const size_t blocks = (D.batch + G::P - 1) / G::P;
     if (k1 != 2) return hipErrorInvalidValue;
+    if constexpr (MODE == 0 && G::P == 1 && FHE_EXT2 && sizeof(W) == 8 && LOGN >= 12) {
+        if (D.level == 1) {
+            hipLaunchKernelGGL((k_extprod2<LOGN, W, NEGA>), dim3((unsigned)D.batch), dim3(G::THREADS), 0, s, D, A);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((k_dmac<LOGN, W, NEGA, 2, false, MODE>), dim3(blocks), dim3(G::THREADS), 0, s, D, A);
     return hipGetLastError();
 }

@@ -334,6 +334,47 @@ def test_external_product_16384(fg, q, bl, lv):
         assert (got[i] == t.external_product(k, bl, lv, glwe[i], ggsw)).all(), i
 
 
+@pytest.mark.parametrize("n,q,bl", [(4096, P62, 20), (8192, P62, 23), (8192, 1152921504606584833, 30),
+                                     (16384, P62, 1)])
+def test_external_product_single_level_vs_oracle(fg, n, q, bl):
+    """Level 1 with 64-bit words runs the paired-transform kernel
+    (k_extprod2): digit(c0) and digit(c1) transformed in lockstep, key MAC in
+    place, both inverses in lockstep.  Raw (non-canonical) GLWE words and
+    the largest / smallest digit bases included."""
+    k, b, lv = 1, 4, 1
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    ggsw = oracle.splitmix_fill(n + bl, q, (k + 1) * lv * (k + 1) * n).reshape((k + 1) * lv, k + 1, n)
+    glwe = oracle.splitmix_fill(n * 3 + bl, q, b * (k + 1) * n).reshape(b, k + 1, n)
+    glwe[1, 0, :4] = [2**64 - 1, q, q - 1, 0]
+    got = fg.ExternalProduct(r, ggsw, bl, lv, k)(glwe)
+    for i in range(b):
+        assert (got[i] == t.external_product(k, bl, lv, glwe[i], ggsw)).all(), i
+
+
+def test_external_product_single_level_negacyclic_is_linear(fg):
+    """Negacyclic mode (no oracle restatement): ExtProd(G, c) computed by the
+    fused kernel equals the composition of the library's own independent
+    kernels -- decompose, forward, pointwise by the prepared key rows, sum,
+    inverse."""
+    import torch
+
+    n, q, bl, lv, k = 8192, P62, 23, 1, 1
+    r = fg.PolynomialRing(n, q, mode="negacyclic")
+    ggsw = oracle.splitmix_fill(5, q, 2 * 2 * n).reshape(2, 2, n)
+    glwe = oracle.splitmix_fill(6, q, 2 * 2 * n).reshape(2, 2, n)
+    got = fg.ExternalProduct(r, ggsw, bl, lv, k)(glwe)
+    for i in range(2):
+        digits = [fg.decompose_polynomial(r, glwe[i, j:j + 1], bl, lv)[0] for j in range(2)]
+        for j in range(2):
+            acc = np.zeros((1, n), np.uint64)
+            for row in range(2):
+                f = r.forward_ntt(np.ascontiguousarray(digits[row].reshape(1, n)))
+                g = r.forward_ntt(np.ascontiguousarray(ggsw[row, j].reshape(1, n)))
+                acc = r.add(acc, r.pointwise_multiply(f, g))
+            assert (got[i, j] == r.inverse_ntt(acc)[0]).all(), (i, j)
+
+
 def test_decompose(fg):
     n, q = 1024, P62
     r = fg.PolynomialRing(n, q)
