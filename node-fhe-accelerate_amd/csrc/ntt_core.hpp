@@ -785,10 +785,11 @@ __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);
     }
 }
-template <int LOGN, bool NEGA, int PF, typename W>
+template <int LOGN, bool NEGA, int PF, typename W, typename F1 = NoFin, typename F2 = NoFin>
 __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
                                           uint64_t *__restrict__ dst, uint64_t *__restrict__ dst2,
-                                          const NttArgs<W> &A, Tw<W> scale, const Tw<W> *__restrict__ post) {
+                                          const NttArgs<W> &A, Tw<W> scale, const Tw<W> *__restrict__ post,
+                                          F1 &&fin1 = NoFin{}, F2 &&fin2 = NoFin{}) {
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
     constexpr int LAST = G::NP - 1;
@@ -809,8 +810,8 @@ __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
             x = A.ar.shoup(x, post[gi]);
             x2 = A.ar.shoup(x2, post[gi]);
         }
-        bstore(r1, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, (uint64_t)A.ar.red1q(x));
-        bstore(r2, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, (uint64_t)A.ar.red1q(x2));
+        bstore(r1, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin1(gi, (uint64_t)A.ar.red1q(x)));
+        bstore(r2, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin2(gi, (uint64_t)A.ar.red1q(x2)));
     }
 }
 
