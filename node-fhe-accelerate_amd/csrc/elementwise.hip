@@ -240,6 +240,90 @@ k_tensor_ntt(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uin
     }
 }
 
+// ---- composed external product / relinearisation (k > 1 or N > 16384) ----
+// out[b][j] = sum_r X[b][r] (.) G[r][kj(j)], X canonical NTT-domain digit
+// transforms, G prepared keys (NTT x R, R = 2^word): Montgomery products
+// remove the R.  kj(j) = j (external product) or K1-1-j (relinearisation:
+// c0' uses b_l, c1' uses a_l).  Canonical output.
+__device__ __forceinline__ uint64_t mont_word(uint64_t a, uint64_t b, uint64_t q, uint64_t qinv, int word) {
+    if (word == 32) {  // a, b < q < 2^30: a*b*2^-32 mod q in [0, 2q)
+        const uint64_t p = a * b;
+        const uint32_t m = (uint32_t)p * (uint32_t)qinv;
+        return (p + (uint64_t)m * q) >> 32;
+    }
+    return mont64(a, b, q, qinv);  // [0, 2q) for q < 2^62
+}
+__global__ void __launch_bounds__(kBlock)
+k_mac_keys(const uint64_t *__restrict__ x, const uint64_t *__restrict__ g, uint64_t *__restrict__ out, uint32_t n,
+           size_t batch, uint32_t rows, uint32_t k1, int swap, int word, ModConsts m) {
+    const size_t total = (size_t)n * batch;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t b = i / n, c = i % n;
+        for (uint32_t j = 0; j < k1; ++j) {
+            const uint32_t kj = swap ? k1 - 1 - j : j;
+            uint64_t acc = 0;
+            for (uint32_t r = 0; r < rows; ++r) {
+                const uint64_t t = mont_word(x[(b * rows + r) * n + c], g[((size_t)r * k1 + kj) * n + c], m.q, m.qinv, word);
+                acc += t;  // < 4q
+                acc = acc >= 2 * m.q ? acc - 2 * m.q : acc;
+            }
+            out[(b * k1 + j) * n + c] = acc >= m.q ? acc - m.q : acc;
+        }
+    }
+}
+// relinearize's digits (encryption.cpp:920-925): d_l = (c2 >> l B) & (2^B - 1)
+// of ct3 [batch][3][n] -> [batch][level][n]
+__global__ void __launch_bounds__(kBlock)
+k_relin_digits(const uint64_t *__restrict__ ct3, uint64_t *__restrict__ out, uint32_t n, size_t batch,
+               uint32_t base_log, uint32_t level) {
+    const size_t total = (size_t)n * batch;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint64_t mask = (1ull << base_log) - 1;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t b = i / n, c = i % n;
+        const uint64_t w = ct3[(3 * b + 2) * n + c];
+        for (uint32_t l = 0; l < level; ++l) out[(b * level + l) * n + c] = (w >> (l * base_log)) & mask;
+    }
+}
+// out[b][j] = mod_add(out[b][j], src[b][j] mod q) for j < rows; out rows
+// [batch][rows][n], src rows [batch][src_rows][n]
+__global__ void __launch_bounds__(kBlock)
+k_add_rows(uint64_t *__restrict__ out, const uint64_t *__restrict__ src, uint32_t n, size_t batch, uint32_t rows,
+           uint32_t src_rows, ModConsts m) {
+    const size_t total = (size_t)n * batch * rows;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t c = i % n, j = (i / n) % rows, b = i / ((size_t)n * rows);
+        const uint64_t a = out[i] < m.q ? out[i] : mod64_slow(out[i], m.q, m.mu);
+        const uint64_t y = red_any(src[(b * src_rows + j) * n + c], m);
+        const uint64_t s = a + y;
+        out[i] = (s < a || s >= m.q) ? s - m.q : s;
+    }
+}
+
+hipError_t launch_mac_keys(const ModConsts &m, int word, const uint64_t *x, const uint64_t *g, uint64_t *out,
+                           uint32_t n, size_t batch, uint32_t rows, uint32_t k1, int swap, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mac_keys, dim3(grid_for((size_t)n * batch)), dim3(kBlock), 0, s, x, g, out, n, batch, rows, k1,
+                       swap, word, m);
+    return hipGetLastError();
+}
+hipError_t launch_relin_digits(const uint64_t *ct3, uint64_t *out, uint32_t n, size_t batch, uint32_t base_log,
+                               uint32_t level, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_relin_digits, dim3(grid_for((size_t)n * batch)), dim3(kBlock), 0, s, ct3, out, n, batch,
+                       base_log, level);
+    return hipGetLastError();
+}
+hipError_t launch_add_rows(const ModConsts &m, uint64_t *out, const uint64_t *src, uint32_t n, size_t batch,
+                           uint32_t rows, uint32_t src_rows, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_add_rows, dim3(grid_for((size_t)n * batch * rows)), dim3(kBlock), 0, s, out, src, n, batch,
+                       rows, src_rows, m);
+    return hipGetLastError();
+}
+
 hipError_t launch_tensor_ntt(const ModConsts &m, const uint64_t *x, const uint64_t *y, uint64_t *out, uint32_t n,
                              size_t batch, hipStream_t s) {
     if (batch == 0) return hipSuccess;

@@ -564,6 +564,65 @@ static int ct_mul_device(fhe_ctx *c, const u64 *x, const u64 *y, u64 *out, size_
     return FHE_OK;
 }
 
+// Composed TFHE external product for shapes the fused kernel does not take
+// (GLWE dimension k > 1, N > 16384): decompose every GLWE row
+// (decompose_polynomial), forward-transform all digit polynomials, the
+// NTT-domain key MAC per output component, inverse.  Bit-identical to the
+// fused kernel and to the reference's per-row inverse-and-add, since every
+// step is exact over Z_q and the inverse is linear.  Device pointers; the
+// digits are staged in chunks of at most ~1 GiB.
+static int extprod_composed(fhe_ctx *c, uint32_t k1, uint32_t level, uint32_t base_log, const u64 *glwe,
+                            const u64 *ggsw, u64 *out, size_t batch) {
+    const size_t n = c->n, rows = (size_t)k1 * level;
+    const size_t per = rows * n * 8;
+    const size_t chunk = std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per));
+    const FHE_NS::ModConsts m = mod_consts(c->q);
+    u64 *dig = nullptr;
+    HIP_TRY(hipMalloc((void **)&dig, chunk * per), "hipMalloc(digits)");
+    int rc = FHE_OK;
+    for (size_t b0 = 0; b0 < batch && rc == FHE_OK; b0 += chunk) {
+        const size_t nb = std::min(chunk, batch - b0);
+        const u64 *g = glwe + b0 * k1 * n;
+        u64 *o = out + b0 * k1 * n;
+        hipError_t e = FHE_NS::launch_decompose(m, g, dig, (u32)n, nb * k1, base_log, level, c->stream);
+        if (e == hipSuccess) e = FHE_NS::launch_fwd(c->plan, dig, dig, nb * rows, 0);
+        if (e == hipSuccess)
+            e = FHE_NS::launch_mac_keys(m, c->word, dig, ggsw, o, (u32)n, nb, (u32)rows, k1, 0, c->stream);
+        if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, o, o, nb * k1);
+        if (e != hipSuccess) rc = hip_fail(e, "composed external product");
+    }
+    (void)hipStreamSynchronize(c->stream);  // dig is freed below
+    (void)hipFree(dig);
+    return rc;
+}
+
+// Composed relinearisation for N > 16384: unsigned LSB-first digits of c2,
+// forward transforms, MAC with the (a_l, b_l) pairs swapped per component,
+// inverse, + c_j.
+static int relin_composed(fhe_ctx *c, uint32_t base_log, uint32_t level, const u64 *ct3, const u64 *rlk, u64 *out,
+                          size_t batch) {
+    const size_t n = c->n, per = (size_t)level * n * 8;
+    const size_t chunk = std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per));
+    const FHE_NS::ModConsts m = mod_consts(c->q);
+    u64 *dig = nullptr;
+    HIP_TRY(hipMalloc((void **)&dig, chunk * per), "hipMalloc(digits)");
+    int rc = FHE_OK;
+    for (size_t b0 = 0; b0 < batch && rc == FHE_OK; b0 += chunk) {
+        const size_t nb = std::min(chunk, batch - b0);
+        const u64 *x = ct3 + b0 * 3 * n;
+        u64 *o = out + b0 * 2 * n;
+        hipError_t e = FHE_NS::launch_relin_digits(x, dig, (u32)n, nb, base_log, level, c->stream);
+        if (e == hipSuccess) e = FHE_NS::launch_fwd(c->plan, dig, dig, nb * level, 0);
+        if (e == hipSuccess) e = FHE_NS::launch_mac_keys(m, c->word, dig, rlk, o, (u32)n, nb, level, 2, 1, c->stream);
+        if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, o, o, nb * 2);
+        if (e == hipSuccess) e = FHE_NS::launch_add_rows(m, o, x, (u32)n, nb, 2, 3, c->stream);
+        if (e != hipSuccess) rc = hip_fail(e, "composed relinearisation");
+    }
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(dig);
+    return rc;
+}
+
 static int relin_device(fhe_ctx *c, uint32_t base_log, uint32_t level, const u64 *ct3, const u64 *rlk, u64 *out,
                         size_t batch) {
     const size_t n = c->n;
@@ -574,6 +633,7 @@ static int relin_device(fhe_ctx *c, uint32_t base_log, uint32_t level, const u64
                 "hipMemcpy2D");
         return FHE_OK;
     }
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN) return relin_composed(c, base_log, level, ct3, rlk, out, batch);
     HIP_TRY(FHE_NS::launch_relin(c->plan, (int)level, (int)base_log, ct3, rlk, out, batch), "relin kernel");
     return FHE_OK;
 }
@@ -848,10 +908,13 @@ int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, ui
     });
 }
 
+// GLWE dimension: the fused kernels take k = 1 (and N <= 16384); other
+// shapes run composed (extprod_composed).
+constexpr uint32_t kMaxGlweDim = 16;
+static bool fused_tfhe(const fhe_ctx *c, uint32_t k) { return k == 1 && (int)c->logn <= FHE_NS::kMaxFusedLogN; }
 static int check_decomp(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level) {
-    if ((int)c->logn > FHE_NS::kMaxFusedLogN)
-        return fail(FHE_ERR_UNSUPPORTED, "external product implemented for degrees up to 16384");
-    if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
+    (void)c;
+    if (k == 0 || k > kMaxGlweDim) return fail(FHE_ERR_UNSUPPORTED, "GLWE dimension k must be between 1 and 16");
     if (level == 0 || base_log == 0 || base_log > 63 || (u64)base_log * level > 64)
         return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
     return FHE_OK;
@@ -860,9 +923,7 @@ static int check_decomp(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_
 int fhe_ggsw_prepare(fhe_ctx *c, uint32_t k, uint32_t level, const uint64_t *ggsw, uint64_t *ggsw_ntt, int where) {
     FHE_MULTI_ONE(where, ggsw, fhe_ggsw_prepare(c, k, level, ggsw, ggsw_ntt, where));
     if (int rc = check_ctx(c)) return rc;
-    if ((int)c->logn > FHE_NS::kMaxFusedLogN)
-        return fail(FHE_ERR_UNSUPPORTED, "external product implemented for degrees up to 16384");
-    if (k != 1) return fail(FHE_ERR_UNSUPPORTED, "external product implemented for GLWE dimension k = 1");
+    if (k == 0 || k > kMaxGlweDim) return fail(FHE_ERR_UNSUPPORTED, "GLWE dimension k must be between 1 and 16");
     if (level == 0) return fail(FHE_ERR_INVALID_ARG, "level must be >= 1");
     const size_t polys = (size_t)(k + 1) * level * (k + 1);
     return run_poly_op(c, ggsw, nullptr, ggsw_ntt, polys, where, c->n, c->n,
@@ -876,6 +937,19 @@ int fhe_external_product_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32
     if (int rc = check_decomp(c, k, base_log, level)) return rc;
     if (!ggsw_ntt && batch) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const size_t per = (size_t)(k + 1) * c->n;
+    if (!fused_tfhe(c, k)) {
+        if (batch == 0) return FHE_OK;
+        if (!glwe || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+        DeviceGuard g(c->device);
+        HostStage hs(c->stream);
+        const size_t bytes = batch * per * 8;
+        FHE_TRY(hs.map(where, glwe, bytes, 1));
+        FHE_TRY(hs.map(where, ggsw_ntt, (size_t)(k + 1) * level * per * 8, 1));
+        FHE_TRY(hs.map(where, out, bytes, 2));
+        if (overlaps(out, bytes, glwe, bytes)) return fail(FHE_ERR_INVALID_ARG, "output must not overlap the input");
+        FHE_TRY(extprod_composed(c, k + 1, level, base_log, glwe, ggsw_ntt, out, batch));
+        return where == FHE_HOST ? hs.finish() : FHE_OK;
+    }
     if (where == FHE_HOST && batch) {
         // the key is shared by every ciphertext: upload it once
         DeviceGuard g(c->device);
@@ -929,7 +1003,6 @@ int fhe_ct_multiply_batch(fhe_ctx *c, const uint64_t *ct1, const uint64_t *ct2, 
 int fhe_relin_key_prepare(fhe_ctx *c, uint32_t level, const uint64_t *rlk, uint64_t *rlk_ntt, int where) {
     FHE_MULTI_ONE(where, rlk, fhe_relin_key_prepare(c, level, rlk, rlk_ntt, where));
     if (int rc = check_ctx(c)) return rc;
-    FHE_TRY(check_fused(c, "relinearisation"));
     return run_poly_op(c, rlk, nullptr, rlk_ntt, (size_t)2 * level, where, c->n, c->n,
                        [&](const u64 *const *d, u64 *o, size_t nb, hipStream_t st) { return FHE_NS::launch_fwd(on(c, st), d[0], o, nb, 1); });
 }
@@ -938,7 +1011,6 @@ int fhe_relinearize_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, const u
                           const uint64_t *rlk_ntt, uint64_t *out, size_t batch, int where) {
     FHE_MULTI(batch, where, ct3, fhe_relinearize_batch(c, base_log, level, ct3 + lo * 3 * c->n, rlk_ntt, out + lo * 2 * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
-    FHE_TRY(check_fused(c, "relinearisation"));
     FHE_TRY(check_relin_decomp(base_log, level));
     if (batch == 0) return FHE_OK;
     if (!ct3 || !out || (level && !rlk_ntt)) return fail(FHE_ERR_INVALID_ARG, "null buffer");
@@ -957,7 +1029,6 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, c
                                 int where) {
     FHE_MULTI(batch, where, ct1, fhe_ct_multiply_relin_batch(c, base_log, level, ct1 + lo * 2 * c->n, ct2 + lo * 2 * c->n, rlk_ntt, out + lo * 2 * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
-    FHE_TRY(check_fused(c, "relinearisation"));
     FHE_TRY(check_relin_decomp(base_log, level));
     if (batch == 0) return FHE_OK;
     if (!ct1 || !ct2 || !out || (level && !rlk_ntt)) return fail(FHE_ERR_INVALID_ARG, "null buffer");
@@ -1214,7 +1285,7 @@ int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, co
                    const uint64_t *ct0, const uint64_t *ct1, uint64_t *out, size_t batch, int where) {
     FHE_MULTI(batch, where, ct0, fhe_cmux_batch(c, k, base_log, level, ggsw_ntt, ct0 + lo * (k + 1) * c->n, ct1 + lo * (k + 1) * c->n, out + lo * (k + 1) * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
-    FHE_TRY(check_tfhe(c, k, base_log, level));
+    FHE_TRY(check_decomp(c, k, base_log, level));
     if (batch == 0) return FHE_OK;
     if (!ggsw_ntt || !ct0 || !ct1 || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
     const size_t n = c->n, bytes = batch * (k + 1) * n * 8;
@@ -1226,8 +1297,24 @@ int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, co
     FHE_TRY(hs.map(where, out, bytes, 2));
     if (overlaps(out, bytes, ct0, bytes) || overlaps(out, bytes, ct1, bytes))
         return fail(FHE_ERR_INVALID_ARG, "output must not overlap the inputs");
-    HIP_TRY(FHE_NS::launch_cmux(c->plan, (int)k + 1, (int)level, (int)base_log, ggsw_ntt, ct0, ct1, out, batch),
-            "cmux kernel");
+    if (fused_tfhe(c, k)) {
+        HIP_TRY(FHE_NS::launch_cmux(c->plan, (int)k + 1, (int)level, (int)base_log, ggsw_ntt, ct0, ct1, out, batch),
+                "cmux kernel");
+    } else {  // ct0 + ExtProd(ct1 - ct0) composed (cmux :520-540)
+        const FHE_NS::ModConsts m = mod_consts(c->q);
+        const size_t cnt = batch * (k + 1) * n;
+        HIP_TRY(FHE_NS::launch_addsub(m, ct1, ct0, out, cnt, 1, c->stream), "sub kernel");
+        u64 *tmp = nullptr;
+        HIP_TRY(hipMalloc((void **)&tmp, bytes), "hipMalloc(cmux)");
+        int rc = extprod_composed(c, k + 1, level, base_log, out, ggsw_ntt, tmp, batch);
+        if (rc == FHE_OK) {
+            hipError_t e = FHE_NS::launch_addsub(m, tmp, ct0, out, cnt, 0, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) rc = hip_fail(e, "add kernel");
+        }
+        (void)hipFree(tmp);
+        FHE_TRY(rc);
+    }
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 

@@ -83,6 +83,14 @@ struct ModConsts {
     uint64_t q, mu, qinv, r2;  // mu = floor(2^64/q); Montgomery R = 2^64
     int fast;                  // q odd and q < 2^63
 };
+// Composed TFHE / BFV paths (k > 1, N > 16384): key MAC of NTT-domain
+// digits, relinearisation digits, row-wise mod_add.
+hipError_t launch_mac_keys(const ModConsts &m, int word, const uint64_t *x, const uint64_t *g, uint64_t *out,
+                           uint32_t n, size_t batch, uint32_t rows, uint32_t k1, int swap, hipStream_t s);
+hipError_t launch_relin_digits(const uint64_t *ct3, uint64_t *out, uint32_t n, size_t batch, uint32_t base_log,
+                               uint32_t level, hipStream_t s);
+hipError_t launch_add_rows(const ModConsts &m, uint64_t *out, const uint64_t *src, uint32_t n, size_t batch,
+                           uint32_t rows, uint32_t src_rows, hipStream_t s);
 hipError_t launch_modmul(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,
                          hipStream_t s);
 hipError_t launch_addsub(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n, int sub,

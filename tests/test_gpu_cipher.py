@@ -212,6 +212,41 @@ def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q,
             assert (got["4096"][i] == exp).all(), i
 
 
+@pytest.mark.parametrize("n,q,bl,lv,k", [(1024, P62, 15, 2, 2), (32768, P62, 23, 1, 1)])
+def test_cmux_composed_vs_oracle(fg, n, q, bl, lv, k):
+    """CMux for k > 1 / N > 16384: ct0 + ExtProd(ct1 - ct0) composed."""
+    b = 2
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    ggsw = rnd(n + 7, q, (k + 1) * lv, k + 1, n)
+    g_ntt = be.prepare_ggsw(ggsw[None])[0]
+    ct0, ct1 = rnd(n + 8, q, b, k + 1, n), rnd(n + 9, q, b, k + 1, n)
+    got = be.cmux(g_ntt, ct0, ct1)
+    for i in range(b):
+        assert (got[i] == t.cmux(k, bl, lv, ggsw, ct0[i], ct1[i])).all(), i
+
+
+@pytest.mark.parametrize("n,q,bl,lv", [(32768, P27, 4, 7), (65536, P62, 20, 3)])
+def test_relinearize_large_degree_vs_oracle(fg, n, q, bl, lv):
+    """Relinearisation above 16384 runs composed (relinearize digits,
+    batched transforms, key MAC, inverse, + c_j)."""
+    b = 2
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    ct3 = rnd(n + bl, q, b, 3, n)
+    ct3[0, 2, :3] = [2**64 - 1, q, 1 << bl]
+    rlk = rnd(n + lv, q, lv, 2, n)
+    eng = fg.EncryptionEngine(r)
+    got = eng.relinearize(ct3, fg.EvaluationKey(r, rlk, bl))
+    for i in range(b):
+        assert (got[i] == t.relinearize(bl, lv, ct3[i], rlk)).all(), i
+    # multiply_relin composes the large-degree ct multiply with it
+    x, y = rnd(n + 1, q, b, 2, n), rnd(n + 2, q, b, 2, n)
+    ek = fg.EvaluationKey(r, rlk, bl)
+    assert (eng.multiply_relin(x, y, ek) == eng.relinearize(eng.multiply(x, y), ek)).all()
+
+
 def test_sample_extract_vs_oracle(fg):
     n, q, k = 1024, P27, 1
     r = fg.PolynomialRing(n, q)

@@ -238,10 +238,27 @@ def test_large_degree_chunk_boundaries(fg):
         assert torch.equal(x, m)
 
 
-def test_large_degree_external_product_unsupported(fg):
-    r = fg.PolynomialRing(32768, P62)
+@pytest.mark.parametrize("n,q,bl,lv,k", [(32768, P62, 23, 1, 1), (65536, P27, 9, 3, 1), (1024, P62, 15, 2, 2),
+                                         (256, 7681, 4, 3, 3), (32768, P27, 10, 2, 2)])
+def test_external_product_composed_vs_oracle(fg, n, q, bl, lv, k):
+    """Shapes the fused kernels do not take -- GLWE dimension k > 1 and
+    N > 16384 -- run composed (decompose, batched forward, key MAC,
+    inverse); bit-exact vs the oracle's reference loop."""
+    b = 2
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    ggsw = oracle.splitmix_fill(n + k, q, (k + 1) * lv * (k + 1) * n).reshape((k + 1) * lv, k + 1, n)
+    glwe = oracle.splitmix_fill(n + k + 1, q, b * (k + 1) * n).reshape(b, k + 1, n)
+    glwe[0, 0, :3] = [2**64 - 1, q, q + 5]
+    got = fg.ExternalProduct(r, ggsw, bl, lv, k)(glwe)
+    for i in range(b):
+        assert (got[i] == t.external_product(k, bl, lv, glwe[i], ggsw)).all(), i
+
+
+def test_glwe_dimension_limits(fg):
+    r = fg.PolynomialRing(1024, P62)
     with pytest.raises(fg.FHEError) as ei:
-        fg.ExternalProduct(r, np.zeros((2, 2, 32768), np.uint64), 23, 1)
+        fg.ExternalProduct(r, np.zeros((18, 18, 1024), np.uint64), 23, 1, k=17)  # k <= 16
     assert ei.value.code == -10
 
 
