@@ -362,7 +362,12 @@ def pmc_traffic(kernel, n, batch, q):
     import glob
 
     logn = n.bit_length() - 1
-    sym = f"{KERNEL_SYMBOL[kernel]}<{logn}, {'unsigned int' if q < (1 << 30) else 'unsigned long'},"
+    word = "unsigned int" if q < (1 << 30) else "unsigned long"
+    sym = f"{KERNEL_SYMBOL[kernel]}<{logn}, {word},"
+    if kernel == "polymul" and q < (1 << 30) and logn in (13, 14):
+        # 32 coefficients per thread, paired forward transforms (geometry key
+        # logN | 5 << 8; ntt_inv.hip k_polymul2)
+        sym = f"k_polymul2<{logn | (5 << 8)}, {word},"
     best = None
     for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
         try:
