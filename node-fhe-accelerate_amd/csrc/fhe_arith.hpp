@@ -21,14 +21,40 @@
 namespace FHE_NS {
 
 __device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
-// 64 x 64 -> high 64.  FHE_MULHI64=1: the middle partial products summed with
-// a 65-bit carry (two full-width mads) instead of two zero-extended halves
-// (the compiler builds those pairs with 3 v_mov per product).
+// 64 x 64 -> high 64.  Variants (lab flag FHE_MULHI64): 0 = __umul64hi (the
+// compiler splits the middle sum into two zero-extended halves: 3 v_mov + a
+// 64-bit add per product); 1/2 = 65-bit middle sum in C (the compiler
+// recomputes the carry with a 64-bit compare); 3 (default) = the carry-out of
+// the v_mad_u64_u32 itself, added with one v_addc.  Measured statically on the
+// q62 C3 kernel (k_ntt_fwd_mul<14, u64>): non-multiply VALU 3180 -> 2763 per
+// wave, multiplies unchanged (1590), no new scratch anywhere.
 #ifndef FHE_MULHI64
-#define FHE_MULHI64 0
+#define FHE_MULHI64 3
 #endif
 __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
-#if FHE_MULHI64
+#if FHE_MULHI64 == 3
+    // The middle sum x0*b1 + (x1*b0 + hi(x0*b0)) reaches 65 bits: its carry
+    // comes out of the v_mad_u64_u32 (SGPR pair) and goes into the high word
+    // through one v_addc (s_nop 1: VALU-written SGPR read by a VALU).
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t m1 = (uint64_t)a1 * b0 + __umulhi(a0, b0);  // < 2^64
+    uint64_t m2, cy;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(m2), "=&s"(cy) : "v"(a0), "v"(b1), "v"(m1));
+    const uint64_t h = (uint64_t)a1 * b1 + (m2 >> 32);
+    uint32_t hh;
+    uint64_t cy2;
+    asm("s_nop 1\n\tv_addc_co_u32_e64 %0, %1, %2, 0, %3"
+        : "=v"(hh), "=s"(cy2) : "v"((uint32_t)(h >> 32)), "s"(cy));
+    (void)cy2;
+    return (uint64_t)(uint32_t)h | ((uint64_t)hh << 32);
+#elif FHE_MULHI64 == 2
+    // middle sum to 65 bits through the carry-out of the 64-bit add
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t m1 = (uint64_t)a1 * b0 + __umulhi(a0, b0);  // < 2^64
+    uint64_t m2;
+    const bool c = __builtin_add_overflow((uint64_t)a0 * b1, m1, &m2);
+    return (uint64_t)a1 * b1 + ((m2 >> 32) | ((uint64_t)c << 32));
+#elif FHE_MULHI64
     const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
     const uint64_t m1 = (uint64_t)a1 * b0 + __umulhi(a0, b0);             // < 2^64
     const unsigned __int128 m2 = (unsigned __int128)((uint64_t)a0 * b1) + m1;  // < 2^65
@@ -40,6 +66,18 @@ __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
 // unsigned min: x - k wraps above x when x < k, so min() keeps x.
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// Lab flags, off by default: the 64-bit Shoup remainder as one mad chain
+// (Arith::lo_chain64; a further 2763 -> 2561 on the q62 C3 kernel, but 28 more
+// kernels with scratch: negacyclic u64 transforms, k_extprod2, k_dmac), and
+// red2q from the borrow of the subtraction (LLVM rebuilds the compare: no
+// change).
+#ifndef FHE_SHOUP64_CHAIN
+#define FHE_SHOUP64_CHAIN 0
+#endif
+#ifndef FHE_RED64_BORROW
+#define FHE_RED64_BORROW 0
+#endif
 
 // Twiddle with its Shoup companion w' = floor(w * 2^W / q).
 template <typename W> struct Tw { W w, wp; };
@@ -57,6 +95,7 @@ struct Arith {
     W r2;         // R^2 mod q, R = 2^W
 
     // x in [0, 2^W): x*w mod q, lazy result in [0, 2q)   (Shoup)
+    template <bool CHAIN = true>
     __device__ __forceinline__ W shoup(W x, W w, W wp) const {
         W h = mulhi(x, wp);
 #ifndef FHE_SHOUP_MAD
@@ -90,11 +129,55 @@ struct Arith {
         } else if constexpr (sizeof(W) == 4 && FHE_SHOUP_MAD) {
             // x*w - h*q (mod 2^32) as one v_mad_u64_u32: h*(2^32 - q) + x*w
             return (W)((uint64_t)h * (uint32_t)(0u - q) + (uint32_t)(x * w));
+        } else if constexpr (sizeof(W) == 8 && FHE_SHOUP64_CHAIN && CHAIN) {
+            return (W)lo_chain64(x, w, h);
         } else {
             return x * w - h * q;
         }
     }
+    // 64-bit x*w - h*q (mod 2^64) as x*w + h*(2^64 - q): six v_mad_u64_u32
+    // and no subtraction.  The two low-word products go through the 64-bit
+    // adder of the mad; the four cross products only feed the high word, so
+    // they accumulate in the low half of a mad (one instruction each instead
+    // of v_mul_lo + v_add3 + the borrow chain of a 64-bit subtract).
+    __device__ __forceinline__ uint64_t lo_chain64(uint64_t x, uint64_t w, uint64_t h) const {
+        const uint64_t nq = 0ull - (uint64_t)q;
+        const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+        const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32);
+        const uint32_t n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
+        uint64_t p = (uint64_t)x0 * w0;
+        p = (uint64_t)h0 * n0 + p;
+        uint32_t acc = madlo(x0, w1, (uint32_t)(p >> 32));
+        acc = madlo(x1, w0, acc);
+        acc = madlo_s(h0, n1, acc);
+        acc = madlo_s(h1, n0, acc);
+        return (uint64_t)(uint32_t)p | ((uint64_t)acc << 32);
+    }
+    // a*b + c (mod 2^32) in one v_mad_u64_u32 (high half of the addend and
+    // of the result unused); _s: b wave-uniform.
+    static __device__ __forceinline__ uint32_t madlo(uint32_t a, uint32_t b, uint32_t c) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 cc;
+        cc.x = c;
+        uint64_t r, cy;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=&s"(cy) : "v"(a), "v"(b), "v"(cc));
+        (void)cy;
+        return (uint32_t)r;
+    }
+    static __device__ __forceinline__ uint32_t madlo_s(uint32_t a, uint32_t b, uint32_t c) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 cc;
+        cc.x = c;
+        uint64_t r, cy;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=&s"(cy) : "v"(a), "s"(b), "v"(cc));
+        (void)cy;
+        return (uint32_t)r;
+    }
     __device__ __forceinline__ W shoup(W x, Tw<W> t) const { return shoup(x, t.w, t.wp); }
+    // Inverse butterflies keep the plain 64-bit form: with the mad chain the
+    // compiler gives the non-negacyclic u64 inverse kernels a 256-byte stack
+    // frame (k_ntt_inv / k_polymul <14, u64>).
+    __device__ __forceinline__ W shoup_inv(W x, Tw<W> t) const { return shoup<false>(x, t.w, t.wp); }
 
     // Montgomery: a*b*R^-1 mod q in [0, 2q); requires a*b < q*R.
     __device__ __forceinline__ W mont(W a, W b) const {
@@ -104,8 +187,16 @@ struct Arith {
         return hi + mulhi(m, q) + (lo != 0 ? W(1) : W(0));
     }
 
-    __device__ __forceinline__ W red2q(W x) const { return umin(x, W(x - q2)); }  // [0,4q)->[0,2q)
-    __device__ __forceinline__ W red1q(W x) const { return umin(x, W(x - q)); }   // [0,2q)->[0,q)
+    __device__ __forceinline__ W red2q(W x) const { return redk(x, q2); }  // [0,4q)->[0,2q)
+    __device__ __forceinline__ W red1q(W x) const { return redk(x, q); }   // [0,2q)->[0,q)
+    static __device__ __forceinline__ W redk(W x, W k) {
+        if constexpr (sizeof(W) == 8 && FHE_RED64_BORROW) {
+            W d;
+            return __builtin_sub_overflow(x, k, &d) ? x : d;
+        } else {
+            return umin(x, W(x - k));
+        }
+    }
     __device__ __forceinline__ W canon4(W x) const { return red1q(red2q(x)); }     // [0,4q)->[0,q)
 
     // 32-bit forward twiddles are stored negated, {-w mod 2^32, w'}
@@ -162,14 +253,14 @@ struct Arith {
         W s = x + y;
         W d = x - y + q2;
         x = red2q(s);
-        y = shoup(d, t);
+        y = shoup_inv(d, t);
     }
     // Last GS stage with the N^-1 scaling folded in (w = 1 at stage 0).
     __device__ __forceinline__ void gs_scaled(W &x, W &y, Tw<W> ninv) const {
         W s = x + y;
         W d = x - y + q2;
-        x = shoup(s, ninv);
-        y = shoup(d, ninv);
+        x = shoup_inv(s, ninv);
+        y = shoup_inv(d, ninv);
     }
 };
 
