@@ -154,7 +154,9 @@ int fhe_poly_mul_scalar_batch(fhe_ctx *ctx, const uint64_t *a, uint64_t scalar, 
  * ggsw:  [(k+1)*level rows][k+1][n], rows ordered as the reference's
  *        ggsw.matrix (mask digit rows first, digit level inner).
  * fhe_ggsw_prepare turns a coefficient-form GGSW into the NTT-domain form
- * fhe_external_product_batch consumes (same shape).  k = 1 is implemented. */
+ * fhe_external_product_batch consumes (same shape).  GLWE dimension k = 1..16:
+ * fused kernels for k = 1 and n <= 16384, composed (decompose, batched
+ * transforms, key MAC, inverse) otherwise. */
 int fhe_ggsw_prepare(fhe_ctx *ctx, uint32_t k, uint32_t level, const uint64_t *ggsw, uint64_t *ggsw_ntt, int where);
 int fhe_external_product_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t level, const uint64_t *glwe,
                                const uint64_t *ggsw_ntt, uint64_t *out, size_t batch, int where);
@@ -211,7 +213,10 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  * fhe_cmux_batch           cmux (:520-540): ct0 + ggsw (x) (ct1 - ct0).
  * fhe_blind_rotate_batch   blind_rotate (:547-577) of acc in place, for each
  *   ciphertext c with its own LWE (lwe_a[c], lwe_b[c]) modulo lwe_q; bsk_ntt
- *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).
+ *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).  k = 1 with
+ *   n <= 16384 runs fused (one launch, or per-step CMux launches); k = 2..16
+ *   and n = 32768 / 65536 run composed step by step (synchronous).
+ *   fhe_bootstrap_batch takes the same shapes.
  * fhe_sample_extract_batch sample_extract (:594-624): lwe_a [batch][k*n].
  * fhe_key_switch_batch     key_switch (:626-674): ksk_a [in_dim*level][out_dim]
  *   (the `first` polynomials of ksk.keys, entry i*level + l), ksk_b

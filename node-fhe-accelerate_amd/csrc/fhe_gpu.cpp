@@ -1263,6 +1263,44 @@ static int check_tfhe(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t 
     return FHE_OK;
 }
 
+// Blind rotation / bootstrap: the fused kernels take k = 1 and N <= 16384;
+// other shapes (k = 2..16, N = 32768 / 65536) run composed step by step.
+static int check_br(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level) {
+    return fused_tfhe(c, k) ? check_tfhe(c, k, base_log, level) : check_decomp(c, k, base_log, level);
+}
+
+// blind_rotate (bootstrap_engine.cpp:547-577) for the shapes without a fused
+// CMux: X^-round(b 2N/q) acc, then per LWE coefficient d = X^r cur - cur,
+// ExtProd(bsk_i, d) composed (decompose, batched transforms, key MAC,
+// inverse), cur + product -- ping-ponging two device buffers; skipped steps
+// (r == 0) copy cur through.  Synchronous on the context stream.
+static int blind_rotate_composed(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
+                                 const u64 *lwe_a, const u64 *lwe_b, uint64_t lwe_q, const u64 *bsk_ntt, u64 *acc,
+                                 size_t batch) {
+    const size_t n = c->n, k1 = k + 1, bytes = batch * k1 * n * 8;
+    const size_t ggsw_words = k1 * level * k1 * n;
+    const FHE_NS::ModConsts m = mod_consts(c->q);
+    StreamTemp tmp(c->stream);
+    u64 *cur = nullptr, *d = nullptr, *ep = nullptr;
+    FHE_TRY(tmp.alloc(bytes, cur));
+    FHE_TRY(tmp.alloc(bytes, d));
+    FHE_TRY(tmp.alloc(bytes, ep));
+    HIP_TRY(FHE_NS::launch_rotate(m, acc, cur, (uint32_t)n, (uint32_t)k1, batch, nullptr, lwe_b, lwe_q, c->stream),
+            "rotate kernel");
+    for (uint32_t i = 0; i < lwe_dim; ++i) {
+        HIP_TRY(FHE_NS::launch_br_diff(m, cur, d, (uint32_t)n, (uint32_t)k1, batch, lwe_a, lwe_dim, i, lwe_q, c->stream),
+                "blind rotate step kernel");
+        FHE_TRY(extprod_composed(c, (uint32_t)k1, level, base_log, d, bsk_ntt + ggsw_words * i, ep, batch));
+        HIP_TRY(FHE_NS::launch_br_add(m, cur, ep, d, (uint32_t)n, (uint32_t)k1, batch, lwe_a, lwe_dim, i, lwe_q,
+                                      c->stream),
+                "blind rotate step kernel");
+        std::swap(cur, d);
+    }
+    HIP_TRY(hipMemcpyAsync(acc, cur, bytes, hipMemcpyDeviceToDevice, c->stream), "hipMemcpyAsync");
+    HIP_TRY(hipStreamSynchronize(c->stream), "blind rotate");
+    return FHE_OK;
+}
+
 int fhe_glwe_rotate_batch(fhe_ctx *c, uint32_t k, const int32_t *rot, const uint64_t *glwe, uint64_t *out,
                           size_t batch, int where) {
     FHE_MULTI(batch, where, glwe, fhe_glwe_rotate_batch(c, k, rot + lo, glwe + lo * (k + 1) * c->n, out + lo * (k + 1) * c->n, nb, where));
@@ -1330,7 +1368,7 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
                            uint64_t *acc, size_t batch, int where) {
     FHE_MULTI(batch, where, acc, fhe_blind_rotate_batch(c, k, base_log, level, lwe_dim, lwe_a + lo * lwe_dim, lwe_b + lo, lwe_q, bsk_ntt, acc + lo * (k + 1) * c->n, nb, where));
     FHE_TRY(check_common(c, where, batch));
-    FHE_TRY(check_tfhe(c, k, base_log, level));
+    FHE_TRY(check_br(c, k, base_log, level));
     if (lwe_q == 0) return fail(FHE_ERR_ZERO_MODULUS, "LWE modulus must be non-zero");
     if (batch == 0) return FHE_OK;
     if (!lwe_b || !acc || (lwe_dim && (!lwe_a || !bsk_ntt))) return fail(FHE_ERR_INVALID_ARG, "null buffer");
@@ -1342,6 +1380,10 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
     FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
     FHE_TRY(hs.map(where, acc, bytes, 3));
+    if (!fused_tfhe(c, k)) {
+        FHE_TRY(blind_rotate_composed(c, k, base_log, level, lwe_dim, lwe_a, lwe_b, lwe_q, bsk_ntt, acc, batch));
+        return where == FHE_HOST ? hs.finish() : FHE_OK;
+    }
     // The whole loop as one launch with the accumulators in LDS
     // (ntt_br.hip); FHE_BR_PERSIST_MAX caps the batch it takes (0 = never).
     const char *pm = std::getenv("FHE_BR_PERSIST_MAX");
@@ -1485,7 +1527,7 @@ int fhe_bootstrap_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t leve
                                                        lwe_q, bsk_ntt, test_poly, ks_base_log, ks_level, out_dim,
                                                        ksk_a, ksk_b, out_a + lo * out_dim, out_b + lo, nb, where));
     FHE_TRY(check_common(c, where, batch));
-    FHE_TRY(check_tfhe(c, k, base_log, level));
+    FHE_TRY(check_br(c, k, base_log, level));
     if (lwe_q == 0) return fail(FHE_ERR_ZERO_MODULUS, "LWE modulus must be non-zero");
     if (ks_base_log == 0 || ks_base_log > 63 || (ks_level > 0 && (u64)(ks_level - 1) * ks_base_log >= 64))
         return fail(FHE_ERR_INVALID_ARG, "invalid key-switch decomposition (base_log, level)");

@@ -108,6 +108,12 @@ hipError_t launch_tensor_ntt(const ModConsts &m, const uint64_t *x, const uint64
 // (blind_rotate's initial rotation by the LWE body).
 hipError_t launch_rotate(const ModConsts &m, const uint64_t *in, uint64_t *out, uint32_t n, uint32_t k1, size_t batch,
                          const int32_t *rot, const uint64_t *lwe_b, uint64_t lwe_q, hipStream_t s);
+// Composed blind-rotation step (lwe.hip k_br_diff / k_br_add)
+hipError_t launch_br_diff(const ModConsts &m, const uint64_t *cur, uint64_t *d, uint32_t n, uint32_t k1, size_t batch,
+                          const uint64_t *lwe_a, uint32_t dim, uint32_t step, uint64_t lwe_q, hipStream_t s);
+hipError_t launch_br_add(const ModConsts &m, const uint64_t *cur, const uint64_t *ep, uint64_t *nxt, uint32_t n,
+                         uint32_t k1, size_t batch, const uint64_t *lwe_a, uint32_t dim, uint32_t step, uint64_t lwe_q,
+                         hipStream_t s);
 // sample_extract: glwe [batch][k+1][n] -> lwe_a [batch][k*n], lwe_b [batch]
 hipError_t launch_sample_extract(const ModConsts &m, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
                                  uint32_t n, uint32_t k, size_t batch, hipStream_t s);

@@ -43,6 +43,41 @@ k_rotate(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint32_t n
     }
 }
 
+// One composed blind-rotation step (GLWE dimension k > 1 or N > 16384, where
+// no fused CMux kernel exists): blind_rotate :565-575 as
+//   d   = X^r cur - cur            (k_br_diff)
+//   nxt = cur + ExtProd(bsk_i, d)  (k_br_add; the external product runs
+//                                   composed in between, fhe_gpu.cpp)
+// with r = round(a_i 2N / q) per ciphertext; r == 0 skips the step (d = 0,
+// nxt = cur word for word, as the reference's `continue`).  The add/sub
+// reduce raw words first, as cmux's mod_sub / mod_add on the reduced inputs.
+__device__ __forceinline__ uint64_t br_sub(uint64_t x, uint64_t y, uint64_t q, uint64_t mu) {
+    return subq(red_q(x, q, mu), red_q(y, q, mu), q);
+}
+__global__ void __launch_bounds__(kLweBlock)
+k_br_diff(const uint64_t *__restrict__ cur, uint64_t *__restrict__ d, uint32_t n, uint32_t k1, size_t batch,
+          const uint64_t *__restrict__ lwe_a, uint32_t dim, uint32_t step, uint64_t lwe_q, uint64_t q, uint64_t mu) {
+    const size_t total = (size_t)batch * k1 * n;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t poly = i / n, c = poly / k1;
+        const int32_t r = rot_amount(lwe_a[c * dim + step], n, lwe_q);
+        d[i] = r == 0 ? 0 : br_sub(rotated_at(cur + poly * n, (uint32_t)(i % n), rot_norm(r, n), n, q, mu), cur[i], q, mu);
+    }
+}
+__global__ void __launch_bounds__(kLweBlock)
+k_br_add(const uint64_t *__restrict__ cur, const uint64_t *__restrict__ ep, uint64_t *__restrict__ nxt, uint32_t n,
+         uint32_t k1, size_t batch, const uint64_t *__restrict__ lwe_a, uint32_t dim, uint32_t step, uint64_t lwe_q,
+         uint64_t q, uint64_t mu) {
+    const size_t total = (size_t)batch * k1 * n;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const size_t c = i / n / k1;
+        const int32_t r = rot_amount(lwe_a[c * dim + step], n, lwe_q);
+        nxt[i] = r == 0 ? cur[i] : addq(red_q(ep[i], q, mu), red_q(cur[i], q, mu), q);
+    }
+}
+
 __global__ void __launch_bounds__(kLweBlock)
 k_sample_extract(const uint64_t *__restrict__ glwe, uint64_t *__restrict__ lwe_a, uint64_t *__restrict__ lwe_b,
                  uint32_t n, uint32_t k, size_t batch, uint64_t q, uint64_t mu) {
@@ -151,6 +186,22 @@ hipError_t launch_rotate(const ModConsts &m, const uint64_t *in, uint64_t *out, 
     if (batch == 0) return hipSuccess;
     hipLaunchKernelGGL(k_rotate, dim3(lwe_grid((size_t)batch * k1 * n)), dim3(kLweBlock), 0, s, in, out, n, k1, batch,
                        rot, lwe_b, lwe_q, m.q, m.mu);
+    return hipGetLastError();
+}
+
+hipError_t launch_br_diff(const ModConsts &m, const uint64_t *cur, uint64_t *d, uint32_t n, uint32_t k1, size_t batch,
+                          const uint64_t *lwe_a, uint32_t dim, uint32_t step, uint64_t lwe_q, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_br_diff, dim3(lwe_grid((size_t)batch * k1 * n)), dim3(kLweBlock), 0, s, cur, d, n, k1, batch,
+                       lwe_a, dim, step, lwe_q, m.q, m.mu);
+    return hipGetLastError();
+}
+hipError_t launch_br_add(const ModConsts &m, const uint64_t *cur, const uint64_t *ep, uint64_t *nxt, uint32_t n,
+                         uint32_t k1, size_t batch, const uint64_t *lwe_a, uint32_t dim, uint32_t step, uint64_t lwe_q,
+                         hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_br_add, dim3(lwe_grid((size_t)batch * k1 * n)), dim3(kLweBlock), 0, s, cur, ep, nxt, n, k1,
+                       batch, lwe_a, dim, step, lwe_q, m.q, m.mu);
     return hipGetLastError();
 }
 

@@ -227,6 +227,51 @@ def test_cmux_composed_vs_oracle(fg, n, q, bl, lv, k):
         assert (got[i] == t.cmux(k, bl, lv, ggsw, ct0[i], ct1[i])).all(), i
 
 
+@pytest.mark.parametrize("n,q,bl,lv,k,dim", [(512, 12289, 4, 3, 2, 6), (1024, P62, 15, 2, 3, 4),
+                                              (32768, P62, 23, 1, 1, 2)])
+def test_blind_rotate_composed_vs_oracle(fg, n, q, bl, lv, k, dim):
+    """Blind rotation where no fused CMux exists (GLWE dimension k > 1,
+    N > 16384): composed steps (X^r acc - acc, composed external product,
+    + acc), bit-exact vs the oracle; skipped steps and a rotation of 2N."""
+    b = 3
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(n + 31, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a = rnd(n + 32, q, b, dim)
+    lwe_a[0, 0] = 0          # rotation 0: the step is skipped
+    lwe_a[0, 1] = q - 1      # rotation 2N: computed
+    lwe_a[1, :] = 0          # every step skipped
+    lwe_b = rnd(n + 33, q, b)
+    acc0 = rnd(n + 34, q, b, k + 1, n)
+    acc = acc0.copy()
+    be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
+    for i in range(b):
+        exp = t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])
+        assert (acc[i] == exp).all(), i
+
+
+def test_bootstrap_glwe_dim2_vs_oracle(fg):
+    """bootstrap_with_test_poly at GLWE dimension k = 2 (composed blind
+    rotation, then sample extract and key switch over k*N mask words)."""
+    n, q, bl, lv, dim, k, b = 512, 12289, 4, 3, 5, 2, 2
+    ks_bl, ks_lv, out_dim = 4, 3, 21
+    r = fg.PolynomialRing(n, q)
+    o = oracle.NTT(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(161, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a, lwe_b = rnd(162, q, b, dim), rnd(163, q, b)
+    lwe_a[0, 0] = 0
+    tp = be.create_lookup_table(lambda x: (3 * x + 1) % 8, 8, 8)
+    ksk_a, ksk_b = rnd(164, q, k * n * ks_lv, out_dim), rnd(165, q, k * n * ks_lv)
+    oa, ob = be.bootstrap(lwe_a, lwe_b, bsk_ntt, tp, ksk_a, ksk_b, ks_bl, ks_lv)
+    for i in range(b):
+        ea, eb = o.bootstrap(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, tp, ks_bl, ks_lv, ksk_a, ksk_b)
+        assert (oa[i] == ea).all() and int(ob[i]) == eb, i
+
+
 @pytest.mark.parametrize("n,q,bl,lv", [(32768, P27, 4, 7), (65536, P62, 20, 3)])
 def test_relinearize_large_degree_vs_oracle(fg, n, q, bl, lv):
     """Relinearisation above 16384 runs composed (relinearize digits,
