@@ -83,7 +83,8 @@ int fhe_detect(fhe_hw_caps *caps);
  * be a power of two in [4, 65536]; the GPU kernels implement every such n
  * and q < 2^62 (FHE_ERR_UNSUPPORTED otherwise).  n > 16384 runs as a
  * two-pass row/column split and the context holds 512 MiB of device
- * scratch; the external product is limited to n <= 16384.
+ * scratch (every entry point takes such contexts: fused kernels up to
+ * n = 16384, composed ones above).
  * device: HIP device ordinal.                                              */
 int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out);
 void fhe_ctx_destroy(fhe_ctx *ctx);
@@ -215,7 +216,8 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  *   ciphertext c with its own LWE (lwe_a[c], lwe_b[c]) modulo lwe_q; bsk_ntt
  *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).  k = 1 with
  *   n <= 16384 runs fused (one launch, or per-step CMux launches); k = 2..16
- *   and n = 32768 / 65536 run composed step by step (synchronous).
+ *   and n = 32768 / 65536 run composed step by step (one digit buffer for
+ *   the whole loop, stream-ordered, no host synchronisation).
  *   fhe_bootstrap_batch takes the same shapes.
  * fhe_sample_extract_batch sample_extract (:594-624): lwe_a [batch][k*n].
  * fhe_key_switch_batch     key_switch (:626-674): ksk_a [in_dim*level][out_dim]
@@ -282,6 +284,72 @@ int fhe_bootstrap_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t le
                         const uint64_t *ksk_a, const uint64_t *ksk_b, uint64_t *out_a, uint64_t *out_b, size_t batch,
                         int where);
 
+/* ---- device randomness and key material (key_manager.cpp, bootstrap_engine.cpp)
+ * SecureRandom's draws (key_manager.cpp:53-115) come from a ChaCha20
+ * keystream (RFC 8439 block function) keyed by seed[4] (256 bits, little-
+ * endian words), with the 64-bit `stream` as the nonce: element i of a
+ * stream of `count` elements draws from blocks i, i + count, i + 2 count, ..
+ * (8 u64 words per block, in order).  The same (seed, stream, count) gives
+ * the same values on every device and in the CPU oracle (oracle_sample), so
+ * keys and encryptions are reproducible; the engine seeds from the OS CSPRNG.
+ *   FHE_SAMPLE_UNIFORM   random_u64_range(q): rejection below (2^64 - q) % q, then % q (:60-71)
+ *   FHE_SAMPLE_TERNARY   sample_ternary: range(3) -> {q-1, 0, 1} (:73-83)
+ *   FHE_SAMPLE_GAUSSIAN  sample_gaussian(std_dev, q): Box-Muller on two 53-bit
+ *                        uniforms, std::round, negatives as q + x (:85-110)
+ *   FHE_SAMPLE_BINARY    sample_binary: random_u64() & 1
+ *   FHE_SAMPLE_RAW       random_u64()
+ * q is the context modulus.  Every keygen entry point names the streams it
+ * takes; results follow the reference formulas under the context's
+ * transform product (*).
+ * fhe_encrypt_sampled_batch   encrypt_internal (encryption.cpp:171-205) with
+ *   u ternary (stream), e1 (stream + 1), e2 (stream + 2) error, [batch][n]
+ *   each; otherwise as fhe_encrypt_batch.
+ * fhe_public_key_generate     generate_public_key (key_manager.cpp:218-246):
+ *   pk [2][n] = (a, a (*) s + e), a uniform (stream), e error (stream + 1).
+ * fhe_eval_key_generate       generate_eval_key (:252-333): rlk [level][2][n],
+ *   a_l uniform (stream + 2l), e_l error (stream + 2l + 1),
+ *   b_l = a_l (*) s + e_l + (s (*) s) * power_l, power_0 = 1,
+ *   power_{l+1} = (power_l * 2^base_log) % q in u64 arithmetic (as the reference).
+ * fhe_ggsw_encrypt_batch      encrypt_ggsw (bootstrap_engine.cpp:268-306) of
+ *   count values (the LWE key of a bootstrapping key, :308-360): out
+ *   [count][(k+1)*level][k+1][n] coefficient form, row (row, l) an
+ *   encrypt_glwe_zero (:190-227; masks uniform (stream), error (stream + 1),
+ *   body = sum_i mask_i (*) s + e) plus (|v| q) >> ((l+1) base_log) (negated
+ *   mod q for v < 0) on coefficient 0 of mask `row` (row < k) or the body.
+ * fhe_ksk_generate            generate_key_switch_key (:367-420): entry
+ *   e = i*level + l (i < n_in, the GLWE key coefficients glwe_sk[i]):
+ *   ksk_a [entries][lwe_dim] uniform (stream), error (stream + 1; std_dev 0
+ *   selects 3.2), ksk_b[e] = ((u64)((<a_e, lwe_sk> + e) % (int64)q)
+ *   + (glwe_sk[i] q) >> ((l+1) base_log)) % q with the reference's int64 /
+ *   u64 wrap-around.  Shift counts >= 64 take the count mod 64.
+ * fhe_lwe_decrypt_batch       LWE decryption under an integer key s [dim]:
+ *   phase = b - sum_j a_j s_j (mod q), values = round(phase t / q) mod t
+ *   (decode_plaintext's rounding, encryption.cpp:133-148).  Each output
+ *   nullable. */
+#define FHE_SAMPLE_UNIFORM 0
+#define FHE_SAMPLE_TERNARY 1
+#define FHE_SAMPLE_GAUSSIAN 2
+#define FHE_SAMPLE_BINARY 3
+#define FHE_SAMPLE_RAW 4
+int fhe_sample_batch(fhe_ctx *ctx, int kind, const uint64_t seed[4], uint64_t stream, double std_dev, uint64_t *out,
+                     size_t count, int where);
+int fhe_encrypt_sampled_batch(fhe_ctx *ctx, uint64_t t, const uint64_t *pk_prep, const uint64_t *values,
+                              const uint64_t seed[4], uint64_t stream, double std_dev, uint64_t *ct, size_t batch,
+                              int where);
+int fhe_public_key_generate(fhe_ctx *ctx, const uint64_t *sk, const uint64_t seed[4], uint64_t stream, double std_dev,
+                            uint64_t *pk, int where);
+int fhe_eval_key_generate(fhe_ctx *ctx, const uint64_t *sk, uint32_t base_log, uint32_t level, const uint64_t seed[4],
+                          uint64_t stream, double std_dev, uint64_t *rlk, int where);
+int fhe_ggsw_encrypt_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t level, const int64_t *values,
+                           size_t count, const uint64_t *sk, const uint64_t seed[4], uint64_t stream, double std_dev,
+                           uint64_t *out, int where);
+int fhe_ksk_generate(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const uint64_t *glwe_sk, uint32_t n_in,
+                     const int64_t *lwe_sk, uint32_t lwe_dim, const uint64_t seed[4], uint64_t stream, double std_dev,
+                     uint64_t *ksk_a, uint64_t *ksk_b, int where);
+int fhe_lwe_decrypt_batch(uint64_t q, uint64_t t, const int64_t *sk, uint32_t dim, const uint64_t *lwe_a,
+                          const uint64_t *lwe_b, uint64_t *values, uint64_t *phase, size_t batch, int where,
+                          int device, void *hip_stream);
+
 /* ---- context-free modular kernels --------------------------------------- */
 /* BarrettReducer::barrett_mul contract (modular_arithmetic.cpp:268-280):
  * c[i] = a[i]*b[i] mod q for any u64 inputs, any q != 0. stream may be NULL. */
@@ -303,6 +371,20 @@ uint64_t fhe_compat_to_montgomery(const uint64_t consts[4], uint64_t a);
 uint64_t fhe_compat_from_montgomery(const uint64_t consts[4], uint64_t a);
 uint64_t fhe_compat_mod_add(uint64_t q, uint64_t a, uint64_t b);
 uint64_t fhe_compat_mod_sub(uint64_t q, uint64_t a, uint64_t b);
+
+/* ---- context-owned device memory (resident ciphertexts and keys) -------
+ * fhe_ctx_alloc / fhe_ctx_free: stream-ordered allocations on the context's
+ * (first) device: a free is ordered after the work already enqueued on the
+ * context stream, and the device pool keeps the memory warm (no device
+ * synchronisation per call).  fhe_ctx_memcpy copies on the context stream:
+ * FHE_COPY_H2D / FHE_COPY_D2H return when the copy is done (ordered after the
+ * context's earlier work), FHE_COPY_D2D is enqueued. */
+#define FHE_COPY_H2D 0
+#define FHE_COPY_D2H 1
+#define FHE_COPY_D2D 2
+int fhe_ctx_alloc(fhe_ctx *ctx, size_t bytes, void **out);
+int fhe_ctx_free(fhe_ctx *ctx, void *ptr);
+int fhe_ctx_memcpy(fhe_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 
 /* ---- device memory helpers (for callers without their own allocator) --- */
 int fhe_dev_alloc(int device, size_t bytes, void **out);

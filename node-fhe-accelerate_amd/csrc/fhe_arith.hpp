@@ -32,7 +32,15 @@ __device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umu
 #define FHE_MULHI64 3
 #endif
 __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
-#if FHE_MULHI64 == 3
+#if FHE_MULHI64 == 4
+    // carry-free: every partial sum stays below 2^64 (lo(m1) and hi(m1) are
+    // added separately), so no carry flag is written or read
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t m1 = (uint64_t)a1 * b0 + (uint64_t)__umulhi(a0, b0);
+    const uint64_t m2 = (uint64_t)a0 * b1 + (uint64_t)(uint32_t)m1;
+    const uint64_t h = (uint64_t)a1 * b1 + (m1 >> 32);
+    return h + (m2 >> 32);
+#elif FHE_MULHI64 == 3
     // The middle sum x0*b1 + (x1*b0 + hi(x0*b0)) reaches 65 bits: its carry
     // comes out of the v_mad_u64_u32 (SGPR pair) and goes into the high word
     // through one v_addc (s_nop 1: VALU-written SGPR read by a VALU).
@@ -66,6 +74,54 @@ __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
 // unsigned min: x - k wraps above x when x < k, so min() keeps x.
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// 64-bit word arithmetic without carry / borrow / compare flags (FHE_U64_NOVCC).
+// On gfx950 every VALU write of VCC (or of an SGPR pair) that a later VALU
+// reads -- the borrow of v_sub_co -> v_subb_co, the v_cmp_lt_u64 -> 2 x
+// v_cndmask of a select -- is padded by the hazard recognizer with s_nop
+// wait states: 4-5 per 64-bit butterfly in the q62 kernels (653 s_nop in the
+// C3 kernel, 1924 in polymul).  Here a 64-bit add is one v_lshl_add_u64, a
+// subtraction a - b is a + ~b + 1 (two v_not_b32 + the add, the +1 folded
+// into a constant), and the conditional subtraction of k (< 2^63) from
+// x (< 2k) selects on the sign bit of x - k with two v_bfi_b32.
+#ifndef FHE_U64_NOVCC
+#define FHE_U64_NOVCC 0
+#endif
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {  // (m & a) | (~m & b)
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+// (lo, hi) -> u64 as one register pair (a bit cast, not shifts and ors that
+// the compiler may lower to two 64-bit adds)
+__device__ __forceinline__ uint64_t pair64(uint32_t lo, uint32_t hi) {
+    u32x2v v;
+    v.x = lo;
+    v.y = hi;
+    return __builtin_bit_cast(uint64_t, v);
+}
+__device__ __forceinline__ uint64_t not64(uint64_t x) {
+    uint32_t lo, hi;
+    asm("v_not_b32 %0, %1" : "=v"(lo) : "v"((uint32_t)x));
+    asm("v_not_b32 %0, %1" : "=v"(hi) : "v"((uint32_t)(x >> 32)));
+    return pair64(lo, hi);
+}
+// A wave-uniform constant the compiler may no longer relate to its source
+// (x + launder(-k) stays a v_lshl_add_u64 instead of being folded back into
+// a borrow-chain subtraction x - k).
+__device__ __forceinline__ uint64_t launder(uint64_t c) {
+    asm("" : "+s"(c));
+    return c;
+}
+// x < 2k, k < 2^63: x - k if x >= k else x
+__device__ __forceinline__ uint64_t redk64(uint64_t x, uint64_t k) {
+    const uint64_t t = x + launder(0ull - k);  // bit 63 set iff x < k
+    const uint32_t m = (uint32_t)((int32_t)(uint32_t)(t >> 32) >> 31);
+    return pair64(bfi32(m, (uint32_t)x, (uint32_t)t), bfi32(m, (uint32_t)(x >> 32), (uint32_t)(t >> 32)));
+}
+// a - b + c (mod 2^64) as a + ~b + (c + 1); c + 1 wave-uniform
+__device__ __forceinline__ uint64_t sub_add64(uint64_t a, uint64_t b, uint64_t c1) { return a + not64(b) + c1; }
 
 // Lab flags, off by default: the 64-bit Shoup remainder as one mad chain
 // (Arith::lo_chain64; a further 2763 -> 2561 on the q62 C3 kernel, but 28 more
@@ -131,6 +187,8 @@ struct Arith {
             return (W)((uint64_t)h * (uint32_t)(0u - q) + (uint32_t)(x * w));
         } else if constexpr (sizeof(W) == 8 && FHE_SHOUP64_CHAIN && CHAIN) {
             return (W)lo_chain64(x, w, h);
+        } else if constexpr (sizeof(W) == 8 && FHE_U64_NOVCC) {
+            return x * w + h * (W)launder(W(0) - q);  // two low products and one v_lshl_add_u64: no borrow
         } else {
             return x * w - h * q;
         }
@@ -180,17 +238,29 @@ struct Arith {
     __device__ __forceinline__ W shoup_inv(W x, Tw<W> t) const { return shoup<false>(x, t.w, t.wp); }
 
     // Montgomery: a*b*R^-1 mod q in [0, 2q); requires a*b < q*R.
+    // 64-bit words (FHE_U64_NOVCC): the signed form (a*b - m*q) / R + q with
+    // m = lo(a*b) * q^-1, whose low halves cancel exactly -- no carry from
+    // the low half (the `lo != 0` compare) and a flag-free subtraction; the
+    // result is congruent and in (0, 2q) (it may differ from the unsigned
+    // form by q; every caller reduces or accepts [0, 2q)).
     __device__ __forceinline__ W mont(W a, W b) const {
         W lo = a * b;
         W hi = mulhi(a, b);
-        W m = lo * qinv;
-        return hi + mulhi(m, q) + (lo != 0 ? W(1) : W(0));
+        if constexpr (sizeof(W) == 8 && FHE_U64_NOVCC) {
+            const W m = lo * (W(0) - qinv);  // qinv = -q^-1: m = lo * q^-1
+            return (W)sub_add64(hi, mulhi(m, q), (uint64_t)q + 1);
+        } else {
+            W m = lo * qinv;
+            return hi + mulhi(m, q) + (lo != 0 ? W(1) : W(0));
+        }
     }
 
     __device__ __forceinline__ W red2q(W x) const { return redk(x, q2); }  // [0,4q)->[0,2q)
     __device__ __forceinline__ W red1q(W x) const { return redk(x, q); }   // [0,2q)->[0,q)
     static __device__ __forceinline__ W redk(W x, W k) {
-        if constexpr (sizeof(W) == 8 && FHE_RED64_BORROW) {
+        if constexpr (sizeof(W) == 8 && FHE_U64_NOVCC) {
+            return (W)redk64(x, k);
+        } else if constexpr (sizeof(W) == 8 && FHE_RED64_BORROW) {
             W d;
             return __builtin_sub_overflow(x, k, &d) ? x : d;
         } else {
@@ -223,8 +293,13 @@ struct Arith {
         } else {
             W b = shoup(y, t);
             x = a + b;
-            y = a - b + q2;
+            y = sub2q(a, b);
         }
+    }
+    // a - b + 2q (b <= 2q): flag-free for 64-bit words
+    __device__ __forceinline__ W sub2q(W a, W b) const {
+        if constexpr (sizeof(W) == 8 && FHE_U64_NOVCC) return (W)sub_add64(a, b, (uint64_t)q2 + 1);
+        else return a - b + q2;
     }
     // Forward butterfly without reducing x: outputs grow by 2q per stage.
     __device__ __forceinline__ void ct_lazy(W &x, W &y, Tw<W> t) const {
@@ -246,19 +321,19 @@ struct Arith {
         W a = shoup(x, r);
         W b = shoup(y, r);
         x = a + b;
-        y = a - b + q2;
+        y = sub2q(a, b);
     }
     // Gentleman-Sande butterfly, values in [0, 2q).
     __device__ __forceinline__ void gs(W &x, W &y, Tw<W> t) const {
         W s = x + y;
-        W d = x - y + q2;
+        W d = sub2q(x, y);
         x = red2q(s);
         y = shoup_inv(d, t);
     }
     // Last GS stage with the N^-1 scaling folded in (w = 1 at stage 0).
     __device__ __forceinline__ void gs_scaled(W &x, W &y, Tw<W> ninv) const {
         W s = x + y;
-        W d = x - y + q2;
+        W d = sub2q(x, y);
         x = shoup_inv(s, ninv);
         y = shoup_inv(d, ninv);
     }

@@ -19,6 +19,7 @@
 
 #include "../../include/fhe_gpu.h"
 #include "fhe_internal.hpp"
+#include "keygen.hpp"
 
 using u64 = uint64_t;
 using u32 = uint32_t;
@@ -95,6 +96,7 @@ struct fhe_ctx {
     hipStream_t own_stream = nullptr, stream = nullptr;
     Tables tab;
     FHE_NS::Plan plan{};
+    FHE_NS::BigSync big_sync;  // plan.big_sync
     std::vector<u64> fwd_tw, inv_tw;  // reference twiddle vectors (host copy)
     // host staging pipeline of the FHE_HOST batch calls (staged()): kSlots
     // slots, each a stream, pinned host buffers and device buffers for two
@@ -244,6 +246,7 @@ void free_tables(fhe_ctx *c) {
     free_pipe(c);
     for (auto &s : c->plan.big_scratch)
         if (s) { (void)hipFree(s); s = nullptr; }
+    if (c->big_sync.done) { (void)hipEventDestroy(c->big_sync.done); c->big_sync.done = nullptr; }
     if (c->br.exec) (void)hipGraphExecDestroy(c->br.exec);
     if (c->br.graph) (void)hipGraphDestroy(c->br.graph);
     c->br = fhe_ctx::BrGraph{};
@@ -472,6 +475,32 @@ int run_poly_op(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, size_t batch, 
 }
 
 // ---------------------------------------------------------------- ciphertext ops
+#define FHE_TRY(expr)                 \
+    do {                              \
+        if (int _rc = (expr)) return _rc; \
+    } while (0)
+
+// Device temporaries of one call, stream-ordered (no device-wide sync).
+class StreamTemp {
+    std::vector<void *> p_;
+    hipStream_t s_;
+
+  public:
+    explicit StreamTemp(hipStream_t s) : s_(s) {}
+    ~StreamTemp() {
+        for (void *x : p_) (void)hipFreeAsync(x, s_);
+    }
+    int alloc(size_t bytes, u64 *&out) {
+        void *d = nullptr;
+        hipError_t e = hipMallocAsync(&d, bytes ? bytes : 8, s_);
+        if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMallocAsync: out of memory");
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+        p_.push_back(d);
+        out = (u64 *)d;
+        return FHE_OK;
+    }
+};
+
 // Host-resident calls of the multi-buffer entry points: every host buffer is
 // copied to a device temporary (inputs) or allocated (outputs), the device
 // path runs, outputs are copied back.  No chunking: these ops are used at
@@ -485,16 +514,19 @@ class HostStage {
   public:
     explicit HostStage(hipStream_t s) : s_(s) {}
     ~HostStage() {
-        for (void *p : allocs_) (void)hipFree(p);
+        for (void *p : allocs_) (void)hipFreeAsync(p, s_);
     }
     // where == FHE_DEVICE: pass through; else stage.  dir: 1 in, 2 out, 3 in/out.
+    // Temporaries come from the device's stream-ordered pool (kept warm by
+    // the release threshold set at context creation): no hipMalloc/hipFree
+    // device synchronisation per call.
     template <typename T>
     int map(int where, T *&ptr, size_t bytes, int dir) {
         if (where == FHE_DEVICE || ptr == nullptr || bytes == 0) return FHE_OK;
         void *d = nullptr;
-        hipError_t e = hipMalloc(&d, bytes);
-        if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMalloc: out of memory");
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(stage)");
+        hipError_t e = hipMallocAsync(&d, bytes, s_);
+        if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMallocAsync: out of memory");
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(stage)");
         allocs_.push_back(d);
         if (dir & 1) HIP_TRY(hipMemcpyAsync(d, (const void *)ptr, bytes, hipMemcpyHostToDevice, s_), "hipMemcpy(H2D)");
         if (dir & 2) back_.push_back({(void *)ptr, d, bytes});
@@ -507,10 +539,6 @@ class HostStage {
         return FHE_OK;
     }
 };
-#define FHE_TRY(expr)                 \
-    do {                              \
-        if (int _rc = (expr)) return _rc; \
-    } while (0)
 
 static bool overlaps(const void *a, size_t an, const void *b, size_t bn) {
     const char *x = (const char *)a, *y = (const char *)b;
@@ -538,15 +566,14 @@ static int check_relin_decomp(uint32_t base_log, uint32_t level) {
 // transforms, tensor, 3 inverse transforms through a temporary.
 static int ct_mul_composed(fhe_ctx *c, const u64 *x, const u64 *y, u64 *out, size_t batch) {
     const size_t n = c->n;
-    void *t = nullptr;
-    HIP_TRY(hipMalloc(&t, batch * 4 * n * 8), "hipMalloc(ct_mul)");
-    u64 *tx = (u64 *)t, *ty = tx + batch * 2 * n;
+    StreamTemp tmp(c->stream);
+    u64 *tx = nullptr;
+    FHE_TRY(tmp.alloc(batch * 4 * n * 8, tx));
+    u64 *ty = tx + batch * 2 * n;
     hipError_t e = FHE_NS::launch_fwd(c->plan, x, tx, batch * 2, 0);
     if (e == hipSuccess) e = FHE_NS::launch_fwd(c->plan, y, ty, batch * 2, 0);
     if (e == hipSuccess) e = FHE_NS::launch_tensor_ntt(mod_consts(c->q), tx, ty, out, c->n, batch, c->stream);
     if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, out, out, batch * 3);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(t);
     if (e != hipSuccess) return hip_fail(e, "ct_multiply");
     return FHE_OK;
 }
@@ -570,17 +597,22 @@ static int ct_mul_device(fhe_ctx *c, const u64 *x, const u64 *y, u64 *out, size_
 // NTT-domain key MAC per output component, inverse.  Bit-identical to the
 // fused kernel and to the reference's per-row inverse-and-add, since every
 // step is exact over Z_q and the inverse is linear.  Device pointers; the
-// digits are staged in chunks of at most ~1 GiB.
+// digits are staged in chunks of at most ~1 GiB, in `dig` when the caller
+// owns a buffer of extprod_digit_words() (the blind-rotation loop: one
+// buffer for every step), else in a stream-ordered temporary.  Asynchronous
+// on the context stream.
+static size_t extprod_digit_words(const fhe_ctx *c, uint32_t k1, uint32_t level, size_t batch) {
+    const size_t per = (size_t)k1 * level * c->n;
+    return std::max<size_t>(1, std::min(batch, ((size_t)1 << 27) / per)) * per;
+}
 static int extprod_composed(fhe_ctx *c, uint32_t k1, uint32_t level, uint32_t base_log, const u64 *glwe,
-                            const u64 *ggsw, u64 *out, size_t batch) {
+                            const u64 *ggsw, u64 *out, size_t batch, u64 *dig = nullptr) {
     const size_t n = c->n, rows = (size_t)k1 * level;
-    const size_t per = rows * n * 8;
-    const size_t chunk = std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per));
+    const size_t chunk = extprod_digit_words(c, k1, level, batch) / (rows * n);
     const FHE_NS::ModConsts m = mod_consts(c->q);
-    u64 *dig = nullptr;
-    HIP_TRY(hipMalloc((void **)&dig, chunk * per), "hipMalloc(digits)");
-    int rc = FHE_OK;
-    for (size_t b0 = 0; b0 < batch && rc == FHE_OK; b0 += chunk) {
+    StreamTemp tmp(c->stream);
+    if (!dig) FHE_TRY(tmp.alloc(chunk * rows * n * 8, dig));
+    for (size_t b0 = 0; b0 < batch; b0 += chunk) {
         const size_t nb = std::min(chunk, batch - b0);
         const u64 *g = glwe + b0 * k1 * n;
         u64 *o = out + b0 * k1 * n;
@@ -589,11 +621,9 @@ static int extprod_composed(fhe_ctx *c, uint32_t k1, uint32_t level, uint32_t ba
         if (e == hipSuccess)
             e = FHE_NS::launch_mac_keys(m, c->word, dig, ggsw, o, (u32)n, nb, (u32)rows, k1, 0, c->stream);
         if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, o, o, nb * k1);
-        if (e != hipSuccess) rc = hip_fail(e, "composed external product");
+        if (e != hipSuccess) return hip_fail(e, "composed external product");
     }
-    (void)hipStreamSynchronize(c->stream);  // dig is freed below
-    (void)hipFree(dig);
-    return rc;
+    return FHE_OK;
 }
 
 // Composed relinearisation for N > 16384: unsigned LSB-first digits of c2,
@@ -604,10 +634,10 @@ static int relin_composed(fhe_ctx *c, uint32_t base_log, uint32_t level, const u
     const size_t n = c->n, per = (size_t)level * n * 8;
     const size_t chunk = std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per));
     const FHE_NS::ModConsts m = mod_consts(c->q);
+    StreamTemp tmp(c->stream);
     u64 *dig = nullptr;
-    HIP_TRY(hipMalloc((void **)&dig, chunk * per), "hipMalloc(digits)");
-    int rc = FHE_OK;
-    for (size_t b0 = 0; b0 < batch && rc == FHE_OK; b0 += chunk) {
+    FHE_TRY(tmp.alloc(chunk * per, dig));
+    for (size_t b0 = 0; b0 < batch; b0 += chunk) {
         const size_t nb = std::min(chunk, batch - b0);
         const u64 *x = ct3 + b0 * 3 * n;
         u64 *o = out + b0 * 2 * n;
@@ -616,11 +646,9 @@ static int relin_composed(fhe_ctx *c, uint32_t base_log, uint32_t level, const u
         if (e == hipSuccess) e = FHE_NS::launch_mac_keys(m, c->word, dig, rlk, o, (u32)n, nb, level, 2, 1, c->stream);
         if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, o, o, nb * 2);
         if (e == hipSuccess) e = FHE_NS::launch_add_rows(m, o, x, (u32)n, nb, 2, 3, c->stream);
-        if (e != hipSuccess) rc = hip_fail(e, "composed relinearisation");
+        if (e != hipSuccess) return hip_fail(e, "composed relinearisation");
     }
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(dig);
-    return rc;
+    return FHE_OK;
 }
 
 static int relin_device(fhe_ctx *c, uint32_t base_log, uint32_t level, const u64 *ct3, const u64 *rlk, u64 *out,
@@ -715,6 +743,17 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
         hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
         if (e != hipSuccess) rc = hip_fail(e, "hipStreamCreate");
     }
+    if (rc == FHE_OK) {
+        // call temporaries (HostStage, StreamTemp) come from the device's
+        // stream-ordered pool; keep up to 8 GiB of it cached across
+        // synchronisations instead of returning it to the driver each time
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+            uint64_t keep = (uint64_t)8 << 30;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        (void)hipGetLastError();
+    }
     if (rc != FHE_OK) {
         free_tables(c);
         delete c;
@@ -726,6 +765,7 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     c->plan.nega = mode;
     c->plan.lazy = c->word == 32 && (u128)(4 + 2 * logn) * q <= ((u128)1 << 32);
     c->plan.stream = c->stream;
+    c->plan.big_sync = &c->big_sync;
     *out = c;
     return FHE_OK;
 }
@@ -792,7 +832,7 @@ int fhe_ctx_set_stream(fhe_ctx *c, void *s) {
         bool hit = false;
         for (fhe_ctx *sub : c->subs)
             if (sub->device == dev) {
-                fhe_ctx_set_stream(sub, s);
+                if (int rc = fhe_ctx_set_stream(sub, s)) return rc;
                 hit = true;
             }
         if (!hit) return fail(FHE_ERR_INVALID_ARG, "stream is not on any device of this context");
@@ -1039,41 +1079,17 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *c, uint32_t base_log, uint32_t level, c
     FHE_TRY(hs.map(where, ct2, batch * 2 * n * 8, 1));
     FHE_TRY(hs.map(where, rlk_ntt, (size_t)level * 2 * n * 8, 1));
     FHE_TRY(hs.map(where, out, batch * 2 * n * 8, 2));
-    u64 *ct3 = nullptr;
-    HIP_TRY(hipMalloc((void **)&ct3, batch * 3 * n * 8), "hipMalloc(ct3)");
-    int rc = ct_mul_device(c, ct1, ct2, ct3, batch, 0);
-    if (rc == FHE_OK) rc = relin_device(c, base_log, level, ct3, rlk_ntt, out, batch);
-    if (rc == FHE_OK && where == FHE_HOST) rc = hs.finish();
-    if (rc == FHE_OK && where == FHE_DEVICE) {
-        hipError_t e = hipStreamSynchronize(c->stream);  // ct3 is freed below
-        if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    {
+        StreamTemp tmp(c->stream);
+        u64 *ct3 = nullptr;
+        FHE_TRY(tmp.alloc(batch * 3 * n * 8, ct3));
+        FHE_TRY(ct_mul_device(c, ct1, ct2, ct3, batch, 0));
+        FHE_TRY(relin_device(c, base_log, level, ct3, rlk_ntt, out, batch));
     }
-    (void)hipFree(ct3);
-    return rc;
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 
 // ---------------------------------------------------------------- EncryptionEngine encrypt / decrypt
-// Device temporaries of one call, stream-ordered (no device-wide sync).
-class StreamTemp {
-    std::vector<void *> p_;
-    hipStream_t s_;
-
-  public:
-    explicit StreamTemp(hipStream_t s) : s_(s) {}
-    ~StreamTemp() {
-        for (void *x : p_) (void)hipFreeAsync(x, s_);
-    }
-    int alloc(size_t bytes, u64 *&out) {
-        void *d = nullptr;
-        hipError_t e = hipMallocAsync(&d, bytes ? bytes : 8, s_);
-        if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMallocAsync: out of memory");
-        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
-        p_.push_back(d);
-        out = (u64 *)d;
-        return FHE_OK;
-    }
-};
-
 int fhe_secret_key_prepare(fhe_ctx *c, const uint64_t *sk, uint64_t *sk_prep, int where) {
     FHE_MULTI_ONE(where, sk, fhe_secret_key_prepare(c, sk, sk_prep, where));
     FHE_TRY(check_common(c, where, 1));
@@ -1187,6 +1203,256 @@ int fhe_add_plain_batch(fhe_ctx *c, uint64_t t, const uint64_t *ct, const uint64
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
 
+// ---------------------------------------------------------------- randomness and key material
+// (keygen.hip): SecureRandom's draws from a seeded ChaCha20 stream, keys and
+// encryptions composed from them and the ring kernels, on the device.
+static FHE_NS::ChaChaKey chacha_key(const uint64_t seed[4]) {
+    FHE_NS::ChaChaKey k;
+    for (int i = 0; i < 4; ++i) {
+        k.k[2 * i] = (uint32_t)seed[i];
+        k.k[2 * i + 1] = (uint32_t)(seed[i] >> 32);
+    }
+    return k;
+}
+static int check_sample(int kind, const uint64_t *seed) {
+    if (!seed) return fail(FHE_ERR_INVALID_ARG, "null seed");
+    if (kind < FHE_SAMPLE_UNIFORM || kind > FHE_SAMPLE_RAW) return fail(FHE_ERR_INVALID_ARG, "unknown sample kind");
+    return FHE_OK;
+}
+
+int fhe_sample_batch(fhe_ctx *c, int kind, const uint64_t seed[4], uint64_t stream, double std_dev, uint64_t *out,
+                     size_t count, int where) {
+    FHE_MULTI_ONE(where, out, fhe_sample_batch(c, kind, seed, stream, std_dev, out, count, where));
+    FHE_TRY(check_common(c, where, count));
+    FHE_TRY(check_sample(kind, seed));
+    if (count == 0) return FHE_OK;
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, out, count * 8, 2));
+    HIP_TRY(FHE_NS::launch_sample(kind, chacha_key(seed), stream, c->q, std_dev, out, count, c->stream), "sample kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_encrypt_sampled_batch(fhe_ctx *c, uint64_t t, const uint64_t *pk_prep, const uint64_t *values,
+                              const uint64_t seed[4], uint64_t stream, double std_dev, uint64_t *ct, size_t batch,
+                              int where) {
+    FHE_MULTI_ONE(where, ct, fhe_encrypt_sampled_batch(c, t, pk_prep, values, seed, stream, std_dev, ct, batch, where));
+    FHE_TRY(check_common(c, where, batch));
+    FHE_TRY(check_fused(c, "encryption"));
+    FHE_TRY(check_sample(FHE_SAMPLE_UNIFORM, seed));
+    if (batch == 0) return FHE_OK;
+    if (!pk_prep || !values || !ct) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n, cnt = batch * n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, pk_prep, 2 * n * 8, 1));
+    FHE_TRY(hs.map(where, values, cnt * 8, 1));
+    FHE_TRY(hs.map(where, ct, 2 * cnt * 8, 2));
+    if (overlaps(ct, 2 * cnt * 8, values, cnt * 8) || overlaps(ct, 2 * cnt * 8, pk_prep, 2 * n * 8))
+        return fail(FHE_ERR_INVALID_ARG, "output must not overlap the inputs");
+    {
+        // encrypt_internal (encryption.cpp:174-180): u ternary, e1 and e2
+        // error polynomials -- streams stream, stream + 1, stream + 2
+        StreamTemp tmp(c->stream);
+        u64 *u = nullptr;
+        FHE_TRY(tmp.alloc(3 * cnt * 8, u));
+        const FHE_NS::ChaChaKey key = chacha_key(seed);
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kTernary, key, stream, c->q, 0, u, cnt, c->stream), "sample kernel");
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kGaussian, key, stream + 1, c->q, std_dev, u + cnt, cnt, c->stream),
+                "sample kernel");
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kGaussian, key, stream + 2, c->q, std_dev, u + 2 * cnt, cnt, c->stream),
+                "sample kernel");
+        HIP_TRY(FHE_NS::launch_encrypt(c->plan, t, pk_prep, values, u, u + cnt, u + 2 * cnt, ct, batch),
+                "encrypt kernel");
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+// r = a (*) b in the context's transform product, one launch pair
+static hipError_t ring_mul(fhe_ctx *c, const u64 *a, const u64 *b, u64 *r, size_t batch) {
+    return FHE_NS::launch_polymul(c->plan, a, b, r, batch);
+}
+
+int fhe_public_key_generate(fhe_ctx *c, const uint64_t *sk, const uint64_t seed[4], uint64_t stream, double std_dev,
+                            uint64_t *pk, int where) {
+    FHE_MULTI_ONE(where, pk, fhe_public_key_generate(c, sk, seed, stream, std_dev, pk, where));
+    FHE_TRY(check_common(c, where, 1));
+    FHE_TRY(check_sample(FHE_SAMPLE_UNIFORM, seed));
+    if (!sk || !pk) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    if (overlaps(sk, c->n * 8, pk, 2 * c->n * 8)) return fail(FHE_ERR_INVALID_ARG, "output must not overlap the key");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, sk, n * 8, 1));
+    FHE_TRY(hs.map(where, pk, 2 * n * 8, 2));
+    {
+        // generate_public_key (key_manager.cpp:218-246): a uniform, e error,
+        // b = from_ntt(to_ntt(a) (.) to_ntt(s)) + e
+        StreamTemp tmp(c->stream);
+        u64 *e = nullptr;
+        FHE_TRY(tmp.alloc(n * 8, e));
+        const FHE_NS::ChaChaKey key = chacha_key(seed);
+        const FHE_NS::ModConsts m = mod_consts(c->q);
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kUniform, key, stream, c->q, 0, pk, n, c->stream), "sample kernel");
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kGaussian, key, stream + 1, c->q, std_dev, e, n, c->stream),
+                "sample kernel");
+        HIP_TRY(ring_mul(c, pk, sk, pk + n, 1), "polymul kernel");
+        HIP_TRY(FHE_NS::launch_addsub(m, pk + n, e, pk + n, n, 0, c->stream), "add kernel");
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_eval_key_generate(fhe_ctx *c, const uint64_t *sk, uint32_t base_log, uint32_t level, const uint64_t seed[4],
+                          uint64_t stream, double std_dev, uint64_t *rlk, int where) {
+    FHE_MULTI_ONE(where, rlk, fhe_eval_key_generate(c, sk, base_log, level, seed, stream, std_dev, rlk, where));
+    FHE_TRY(check_common(c, where, 1));
+    FHE_TRY(check_sample(FHE_SAMPLE_UNIFORM, seed));
+    if (base_log == 0 || base_log > 63) return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    if (level == 0) return FHE_OK;
+    if (!sk || !rlk) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, sk, n * 8, 1));
+    FHE_TRY(hs.map(where, rlk, (size_t)level * 2 * n * 8, 2));
+    {
+        // generate_eval_key (key_manager.cpp:252-333): s^2 = s (*) s; level l:
+        // a_l uniform (stream + 2l), e_l error (stream + 2l + 1),
+        // b_l = a_l (*) s + e_l + s^2 * base^l, with the reference's u64
+        // power update power = (power * base) % q
+        StreamTemp tmp(c->stream);
+        u64 *s2 = nullptr, *e = nullptr, *sc = nullptr;
+        FHE_TRY(tmp.alloc(n * 8, s2));
+        FHE_TRY(tmp.alloc(n * 8, e));
+        FHE_TRY(tmp.alloc(n * 8, sc));
+        const FHE_NS::ChaChaKey key = chacha_key(seed);
+        const FHE_NS::ModConsts m = mod_consts(c->q);
+        HIP_TRY(ring_mul(c, sk, sk, s2, 1), "polymul kernel");
+        const u64 base = 1ull << base_log;
+        u64 power = 1;
+        for (uint32_t l = 0; l < level; ++l) {
+            u64 *a = rlk + (size_t)2 * l * n, *b = a + n;
+            HIP_TRY(FHE_NS::launch_sample(FHE_NS::kUniform, key, stream + 2 * l, c->q, 0, a, n, c->stream),
+                    "sample kernel");
+            HIP_TRY(FHE_NS::launch_sample(FHE_NS::kGaussian, key, stream + 2 * l + 1, c->q, std_dev, e, n, c->stream),
+                    "sample kernel");
+            HIP_TRY(ring_mul(c, a, sk, b, 1), "polymul kernel");
+            HIP_TRY(FHE_NS::launch_addsub(m, b, e, b, n, 0, c->stream), "add kernel");
+            const u64 sp = power % c->q;  // multiply_scalar's (a * (s % q)) % q
+            HIP_TRY(FHE_NS::launch_mul_scalar(m, s2, sp, (u64)(((u128)sp << 64) / c->q), sc, n, c->stream),
+                    "scalar kernel");
+            HIP_TRY(FHE_NS::launch_addsub(m, b, sc, b, n, 0, c->stream), "add kernel");
+            power = (power * base) % c->q;  // u64 product, as the reference
+        }
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_ggsw_encrypt_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, const int64_t *values,
+                           size_t count, const uint64_t *sk, const uint64_t seed[4], uint64_t stream, double std_dev,
+                           uint64_t *out, int where) {
+    FHE_MULTI_ONE(where, out, fhe_ggsw_encrypt_batch(c, k, base_log, level, values, count, sk, seed, stream, std_dev,
+                                                     out, where));
+    FHE_TRY(check_common(c, where, count));
+    FHE_TRY(check_sample(FHE_SAMPLE_UNIFORM, seed));
+    if (k == 0 || k > kMaxGlweDim) return fail(FHE_ERR_UNSUPPORTED, "GLWE dimension k must be between 1 and 16");
+    if (level == 0 || base_log == 0 || base_log > 63) return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    if (count == 0) return FHE_OK;
+    if (!values || !sk || !out) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    const size_t n = c->n, rows = count * (k + 1) * level;
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, values, count * 8, 1));
+    FHE_TRY(hs.map(where, sk, n * 8, 1));
+    FHE_TRY(hs.map(where, out, rows * (k + 1) * n * 8, 2));
+    {
+        // encrypt_ggsw (bootstrap_engine.cpp:268-306): per row an
+        // encrypt_glwe_zero (:190-227) -- masks uniform (stream), error
+        // (stream + 1), body = sum_i mask_i (*) s + e -- plus the gadget term
+        StreamTemp tmp(c->stream);
+        u64 *masks = nullptr, *prod = nullptr, *err = nullptr, *fs = nullptr;
+        FHE_TRY(tmp.alloc(rows * k * n * 8, masks));
+        FHE_TRY(tmp.alloc(rows * k * n * 8, prod));
+        FHE_TRY(tmp.alloc(rows * n * 8, err));
+        FHE_TRY(tmp.alloc(n * 8, fs));
+        const FHE_NS::ChaChaKey key = chacha_key(seed);
+        const FHE_NS::ModConsts m = mod_consts(c->q);
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kUniform, key, stream, c->q, 0, masks, rows * k * n, c->stream),
+                "sample kernel");
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kGaussian, key, stream + 1, c->q, std_dev, err, rows * n, c->stream),
+                "sample kernel");
+        HIP_TRY(FHE_NS::launch_fwd(c->plan, sk, fs, 1, 0), "fwd kernel");
+        HIP_TRY(FHE_NS::launch_fwd(c->plan, masks, prod, rows * k, 0), "fwd kernel");
+        HIP_TRY(FHE_NS::launch_modmul_bcast(m, prod, fs, prod, (uint32_t)n, rows * k, c->stream), "modmul kernel");
+        HIP_TRY(FHE_NS::launch_inv(c->plan, prod, prod, rows * k), "inv kernel");
+        HIP_TRY(FHE_NS::launch_ggsw_finish(m, prod, masks, err, values, out, (uint32_t)n, k, level, base_log, count,
+                                           c->stream),
+                "ggsw kernel");
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_ksk_generate(fhe_ctx *c, uint32_t base_log, uint32_t level, const uint64_t *glwe_sk, uint32_t n_in,
+                     const int64_t *lwe_sk, uint32_t lwe_dim, const uint64_t seed[4], uint64_t stream, double std_dev,
+                     uint64_t *ksk_a, uint64_t *ksk_b, int where) {
+    FHE_MULTI_ONE(where, ksk_b, fhe_ksk_generate(c, base_log, level, glwe_sk, n_in, lwe_sk, lwe_dim, seed, stream,
+                                                 std_dev, ksk_a, ksk_b, where));
+    FHE_TRY(check_common(c, where, 1));
+    FHE_TRY(check_sample(FHE_SAMPLE_UNIFORM, seed));
+    if (base_log == 0 || base_log > 63) return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
+    const size_t entries = (size_t)n_in * level;
+    if (entries == 0) return FHE_OK;
+    if (!glwe_sk || !ksk_b || (lwe_dim && (!lwe_sk || !ksk_a))) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    DeviceGuard g(c->device);
+    HostStage hs(c->stream);
+    FHE_TRY(hs.map(where, glwe_sk, (size_t)n_in * 8, 1));
+    FHE_TRY(hs.map(where, lwe_sk, (size_t)lwe_dim * 8, 1));
+    FHE_TRY(hs.map(where, ksk_a, entries * lwe_dim * 8, 2));
+    FHE_TRY(hs.map(where, ksk_b, entries * 8, 2));
+    {
+        // generate_key_switch_key (bootstrap_engine.cpp:367-420): entry
+        // e = i L + l: a_e uniform (stream), error (stream + 1)
+        StreamTemp tmp(c->stream);
+        u64 *err = nullptr;
+        FHE_TRY(tmp.alloc(entries * 8, err));
+        const FHE_NS::ChaChaKey key = chacha_key(seed);
+        const FHE_NS::ModConsts m = mod_consts(c->q);
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kUniform, key, stream, c->q, 0, ksk_a, entries * lwe_dim, c->stream),
+                "sample kernel");
+        HIP_TRY(FHE_NS::launch_sample(FHE_NS::kGaussian, key, stream + 1, c->q, std_dev > 0 ? std_dev : 3.2, err,
+                                      entries, c->stream),
+                "sample kernel");
+        HIP_TRY(FHE_NS::launch_ksk_body(m, glwe_sk, lwe_sk, ksk_a, err, ksk_b, n_in, level, base_log, lwe_dim,
+                                        c->stream),
+                "ksk kernel");
+    }
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
+int fhe_lwe_decrypt_batch(uint64_t q, uint64_t t, const int64_t *sk, uint32_t dim, const uint64_t *lwe_a,
+                          const uint64_t *lwe_b, uint64_t *values, uint64_t *phase, size_t batch, int where, int device,
+                          void *stream) {
+    if (q < 2) return fail(FHE_ERR_ZERO_MODULUS, "LWE modulus must be >= 2");
+    if (where != FHE_HOST && where != FHE_DEVICE) return fail(FHE_ERR_INVALID_ARG, "where must be FHE_HOST or FHE_DEVICE");
+    if (batch == 0) return FHE_OK;
+    if (!lwe_b || (dim && (!sk || !lwe_a))) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(FHE_ERR_DEVICE, "no HIP device available (the backend has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(FHE_ERR_INVALID_ARG, "device ordinal out of range");
+    DeviceGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    HostStage hs(s);
+    FHE_TRY(hs.map(where, sk, (size_t)dim * 8, 1));
+    FHE_TRY(hs.map(where, lwe_a, batch * dim * 8, 1));
+    FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
+    FHE_TRY(hs.map(where, values, batch * 8, 2));
+    FHE_TRY(hs.map(where, phase, batch * 8, 2));
+    HIP_TRY(FHE_NS::launch_lwe_decrypt(q, t, sk, dim, lwe_a, lwe_b, values, phase, batch, s), "lwe decrypt kernel");
+    return where == FHE_HOST ? hs.finish() : FHE_OK;
+}
+
 // ---------------------------------------------------------------- RNS ring
 struct fhe_rns_ctx {
     std::vector<fhe_ctx *> limbs;
@@ -1273,7 +1539,8 @@ static int check_br(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t le
 // CMux: X^-round(b 2N/q) acc, then per LWE coefficient d = X^r cur - cur,
 // ExtProd(bsk_i, d) composed (decompose, batched transforms, key MAC,
 // inverse), cur + product -- ping-ponging two device buffers; skipped steps
-// (r == 0) copy cur through.  Synchronous on the context stream.
+// (r == 0) copy cur through.  Every temporary (one digit buffer for all
+// steps) is allocated once, stream-ordered; nothing synchronises the host.
 static int blind_rotate_composed(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
                                  const u64 *lwe_a, const u64 *lwe_b, uint64_t lwe_q, const u64 *bsk_ntt, u64 *acc,
                                  size_t batch) {
@@ -1281,23 +1548,23 @@ static int blind_rotate_composed(fhe_ctx *c, uint32_t k, uint32_t base_log, uint
     const size_t ggsw_words = k1 * level * k1 * n;
     const FHE_NS::ModConsts m = mod_consts(c->q);
     StreamTemp tmp(c->stream);
-    u64 *cur = nullptr, *d = nullptr, *ep = nullptr;
+    u64 *cur = nullptr, *d = nullptr, *ep = nullptr, *dig = nullptr;
     FHE_TRY(tmp.alloc(bytes, cur));
     FHE_TRY(tmp.alloc(bytes, d));
     FHE_TRY(tmp.alloc(bytes, ep));
+    FHE_TRY(tmp.alloc(extprod_digit_words(c, (uint32_t)k1, level, batch) * 8, dig));
     HIP_TRY(FHE_NS::launch_rotate(m, acc, cur, (uint32_t)n, (uint32_t)k1, batch, nullptr, lwe_b, lwe_q, c->stream),
             "rotate kernel");
     for (uint32_t i = 0; i < lwe_dim; ++i) {
         HIP_TRY(FHE_NS::launch_br_diff(m, cur, d, (uint32_t)n, (uint32_t)k1, batch, lwe_a, lwe_dim, i, lwe_q, c->stream),
                 "blind rotate step kernel");
-        FHE_TRY(extprod_composed(c, (uint32_t)k1, level, base_log, d, bsk_ntt + ggsw_words * i, ep, batch));
+        FHE_TRY(extprod_composed(c, (uint32_t)k1, level, base_log, d, bsk_ntt + ggsw_words * i, ep, batch, dig));
         HIP_TRY(FHE_NS::launch_br_add(m, cur, ep, d, (uint32_t)n, (uint32_t)k1, batch, lwe_a, lwe_dim, i, lwe_q,
                                       c->stream),
                 "blind rotate step kernel");
         std::swap(cur, d);
     }
     HIP_TRY(hipMemcpyAsync(acc, cur, bytes, hipMemcpyDeviceToDevice, c->stream), "hipMemcpyAsync");
-    HIP_TRY(hipStreamSynchronize(c->stream), "blind rotate");
     return FHE_OK;
 }
 
@@ -1342,16 +1609,11 @@ int fhe_cmux_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, co
         const FHE_NS::ModConsts m = mod_consts(c->q);
         const size_t cnt = batch * (k + 1) * n;
         HIP_TRY(FHE_NS::launch_addsub(m, ct1, ct0, out, cnt, 1, c->stream), "sub kernel");
+        StreamTemp st(c->stream);
         u64 *tmp = nullptr;
-        HIP_TRY(hipMalloc((void **)&tmp, bytes), "hipMalloc(cmux)");
-        int rc = extprod_composed(c, k + 1, level, base_log, out, ggsw_ntt, tmp, batch);
-        if (rc == FHE_OK) {
-            hipError_t e = FHE_NS::launch_addsub(m, tmp, ct0, out, cnt, 0, c->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-            if (e != hipSuccess) rc = hip_fail(e, "add kernel");
-        }
-        (void)hipFree(tmp);
-        FHE_TRY(rc);
+        FHE_TRY(st.alloc(bytes, tmp));
+        FHE_TRY(extprod_composed(c, k + 1, level, base_log, out, ggsw_ntt, tmp, batch));
+        HIP_TRY(FHE_NS::launch_addsub(m, tmp, ct0, out, cnt, 0, c->stream), "add kernel");
     }
     return where == FHE_HOST ? hs.finish() : FHE_OK;
 }
@@ -1749,6 +2011,44 @@ uint64_t fhe_compat_mod_add(uint64_t q, uint64_t a, uint64_t b) {
 uint64_t fhe_compat_mod_sub(uint64_t q, uint64_t a, uint64_t b) {
     a %= q; b %= q;
     return a >= b ? a - b : q - (b - a);
+}
+
+// ---------------------------------------------------------------- context-owned device memory
+// Stream-ordered allocations on a context's (first) device for callers that
+// keep ciphertexts and keys resident (the N-API DeviceBuffer handles): the
+// pool keeps freed blocks warm, and a free is ordered after all work already
+// enqueued on the context stream, so no device-wide synchronisation.
+int fhe_ctx_alloc(fhe_ctx *c, size_t bytes, void **out) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!out) return fail(FHE_ERR_INVALID_ARG, "null out");
+    fhe_ctx *s = c->multi() ? c->subs[0] : c;
+    DeviceGuard g(s->device);
+    hipError_t e = hipMallocAsync(out, bytes ? bytes : 8, s->stream);
+    if (e == hipErrorOutOfMemory) return fail(FHE_ERR_OOM, "hipMallocAsync: out of memory");
+    HIP_TRY(e, "hipMallocAsync");
+    return FHE_OK;
+}
+int fhe_ctx_free(fhe_ctx *c, void *p) {
+    if (int rc = check_ctx(c)) return rc;
+    if (!p) return FHE_OK;
+    fhe_ctx *s = c->multi() ? c->subs[0] : c;
+    DeviceGuard g(s->device);
+    HIP_TRY(hipFreeAsync(p, s->stream), "hipFreeAsync");
+    return FHE_OK;
+}
+int fhe_ctx_memcpy(fhe_ctx *c, void *dst, const void *src, size_t bytes, int kind) {
+    if (int rc = check_ctx(c)) return rc;
+    if (bytes == 0) return FHE_OK;
+    if (!dst || !src) return fail(FHE_ERR_INVALID_ARG, "null buffer");
+    fhe_ctx *s = c->multi() ? c->subs[0] : c;
+    DeviceGuard g(s->device);
+    const hipMemcpyKind k = kind == FHE_COPY_H2D ? hipMemcpyHostToDevice
+                          : kind == FHE_COPY_D2H ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    if (kind != FHE_COPY_H2D && kind != FHE_COPY_D2H && kind != FHE_COPY_D2D)
+        return fail(FHE_ERR_INVALID_ARG, "unknown copy kind");
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, s->stream), "hipMemcpyAsync");
+    if (kind != FHE_COPY_D2D) HIP_TRY(hipStreamSynchronize(s->stream), "hipStreamSynchronize");
+    return FHE_OK;
 }
 
 // ---------------------------------------------------------------- memory / events

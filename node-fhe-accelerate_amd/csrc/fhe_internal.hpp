@@ -5,9 +5,22 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "ntt_core.hpp"
 
 namespace FHE_NS {
+
+// Orders every use of a context's big-N scratch (Plan::big_scratch): the
+// launch sequence of one two-pass transform is enqueued under `mu`, and a
+// sequence on another stream first waits for `done`, the completion of the
+// previous one.  Host threads and streams (the staging slots, async N-API
+// jobs, a caller's own stream) may then share one context.
+struct BigSync {
+    std::mutex mu;
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+};
 
 struct Plan {
     uint32_t logn;
@@ -18,6 +31,7 @@ struct Plan {
     // N > 2^kMaxFusedLogN (ntt_big.hip): two chunk-sized scratch buffers
     uint64_t *big_scratch[2];
     size_t big_chunk;  // polynomials per scratch chunk
+    BigSync *big_sync; // owned by the context
     NttArgs<uint32_t> a32;
     NttArgs<uint64_t> a64;
 };

@@ -242,11 +242,26 @@ static hipError_t big_dispatch(const Plan &p, const NttArgs<W> &A, int op, const
 
 hipError_t launch_big(const Plan &p, int op, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch) {
     if (batch == 0) return hipSuccess;
+    if (!p.big_sync) return hipErrorInvalidValue;
+    // The scratch pair is shared by every stream of the context: enqueue the
+    // whole sequence under the lock, after the previous sequence if that ran
+    // on another stream.
+    BigSync &bs = *p.big_sync;
+    std::lock_guard<std::mutex> lk(bs.mu);
+    hipError_t e = hipSuccess;
+    if (!bs.done) e = hipEventCreateWithFlags(&bs.done, hipEventDisableTiming);
+    else if (bs.last != p.stream) e = hipStreamWaitEvent(p.stream, bs.done, 0);
+    if (e != hipSuccess) return e;
     if (p.word == 32)
-        return p.nega ? big_dispatch<uint32_t, true>(p, p.a32, op, a, b, c, batch)
-                      : big_dispatch<uint32_t, false>(p, p.a32, op, a, b, c, batch);
-    return p.nega ? big_dispatch<uint64_t, true>(p, p.a64, op, a, b, c, batch)
-                  : big_dispatch<uint64_t, false>(p, p.a64, op, a, b, c, batch);
+        e = p.nega ? big_dispatch<uint32_t, true>(p, p.a32, op, a, b, c, batch)
+                   : big_dispatch<uint32_t, false>(p, p.a32, op, a, b, c, batch);
+    else
+        e = p.nega ? big_dispatch<uint64_t, true>(p, p.a64, op, a, b, c, batch)
+                   : big_dispatch<uint64_t, false>(p, p.a64, op, a, b, c, batch);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(bs.done, p.stream);
+    bs.last = p.stream;
+    return e;
 }
 
 }  // namespace FHE_NS

@@ -2,6 +2,13 @@
 // ntt_processor.cpp:262-311), Montgomery-prepared, and forward + pointwise
 // modmul (config C3: to_ntt then PolynomialRing::pointwise_multiply,
 // polynomial_ring.cpp:104-116, 493-530).
+// Flag-free 64-bit arithmetic (fhe_arith.hpp FHE_U64_NOVCC) in this
+// translation unit: q62 C3 8.75 -> 8.15 ms per 65,536 polys on MI355X
+// (profiles/r3b/ab_novcc.txt; parity tests green).  Each .hip file is its own
+// device code object, so other files keep their own choice.
+#ifndef FHE_U64_NOVCC
+#define FHE_U64_NOVCC 1
+#endif
 #include "fhe_internal.hpp"
 
 namespace FHE_NS {

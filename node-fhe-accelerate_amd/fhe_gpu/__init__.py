@@ -147,6 +147,17 @@ SIGNATURES = [
     ("fhe_bootstrap_batch", C.c_int,
      [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint64, vp, vp, C.c_uint32, C.c_uint32,
       C.c_uint32, vp, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_sample_batch", C.c_int, [vp, C.c_int, u64p, C.c_uint64, C.c_double, vp, C.c_size_t, C.c_int]),
+    ("fhe_encrypt_sampled_batch", C.c_int,
+     [vp, C.c_uint64, vp, vp, u64p, C.c_uint64, C.c_double, vp, C.c_size_t, C.c_int]),
+    ("fhe_public_key_generate", C.c_int, [vp, vp, u64p, C.c_uint64, C.c_double, vp, C.c_int]),
+    ("fhe_eval_key_generate", C.c_int, [vp, vp, C.c_uint32, C.c_uint32, u64p, C.c_uint64, C.c_double, vp, C.c_int]),
+    ("fhe_ggsw_encrypt_batch", C.c_int,
+     [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_size_t, vp, u64p, C.c_uint64, C.c_double, vp, C.c_int]),
+    ("fhe_ksk_generate", C.c_int,
+     [vp, C.c_uint32, C.c_uint32, vp, C.c_uint32, vp, C.c_uint32, u64p, C.c_uint64, C.c_double, vp, vp, C.c_int]),
+    ("fhe_lwe_decrypt_batch", C.c_int,
+     [C.c_uint64, C.c_uint64, vp, C.c_uint32, vp, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
     ("fhe_modmul_batch", C.c_int, [C.c_uint64, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
     ("fhe_ml_constants", C.c_int, [u64p, u64p]),
     ("fhe_ml_montmul_batch", C.c_int, [u64p, vp, vp, vp, C.c_size_t, C.c_int, C.c_int, vp]),
@@ -156,6 +167,9 @@ SIGNATURES = [
     ("fhe_compat_from_montgomery", C.c_uint64, [u64p, C.c_uint64]),
     ("fhe_compat_mod_add", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
     ("fhe_compat_mod_sub", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("fhe_ctx_alloc", C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
+    ("fhe_ctx_free", C.c_int, [vp, vp]),
+    ("fhe_ctx_memcpy", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
     ("fhe_dev_alloc", C.c_int, [C.c_int, C.c_size_t, C.POINTER(vp)]),
     ("fhe_dev_free", C.c_int, [vp]),
     ("fhe_memcpy_h2d", C.c_int, [vp, vp, C.c_size_t]),
@@ -648,6 +662,132 @@ class PublicKey:
         _check(lib().fhe_public_key_prepare(ring._h, bi.ptr, bo.ptr, w))
 
 
+SAMPLE_UNIFORM, SAMPLE_TERNARY, SAMPLE_GAUSSIAN, SAMPLE_BINARY, SAMPLE_RAW = range(5)
+
+
+def _seed_arr(seed):
+    """A 256-bit ChaCha20 seed as 4 u64 words (an int, 4 ints, or bytes)."""
+    if isinstance(seed, (bytes, bytearray)):
+        seed = np.frombuffer(bytes(seed).ljust(32, b"\0")[:32], dtype=np.uint64)
+    elif isinstance(seed, int):
+        seed = [(seed >> (64 * i)) & ((1 << 64) - 1) for i in range(4)]
+    a = (C.c_uint64 * 4)(*[int(x) for x in np.asarray(seed, dtype=np.uint64).reshape(4)])
+    return a
+
+
+def new_seed() -> bytes:
+    """256 bits from the OS CSPRNG (the engine's default seed)."""
+    return os.urandom(32)
+
+
+def sample(ring: "NTTProcessor", kind: int, seed, stream: int, count: int, std_dev: float = 3.2, out=None,
+           device_out: bool = False):
+    """SecureRandom draws (key_manager.cpp:53-115) over the seeded ChaCha20
+    stream of include/fhe_gpu.h (fhe_sample_batch), modulo the ring modulus."""
+    if out is None:
+        out = (torch.empty(count, dtype=torch.int64, device=f"cuda:{ring.device}") if device_out
+               else np.empty(count, dtype=np.uint64))
+    bo = _Buf(out, True)
+    w = _where(bo)
+    ring._bind_stream(w)
+    _check(lib().fhe_sample_batch(ring._h, int(kind), _seed_arr(seed), int(stream), float(std_dev), bo.ptr, count, w))
+    return out
+
+
+class KeyGenerator:
+    """KeyManager (key_manager.cpp:150-333) and the bootstrapping-key half of
+    BootstrapEngine (bootstrap_engine.cpp:268-420) on the GPU, drawing from
+    a seeded ChaCha20 stream: the same (seed, stream) gives the same keys on
+    every device and in the CPU oracle.  Arrays follow the placement of the
+    inputs (numpy: host, torch: device)."""
+
+    def __init__(self, ring: "PolynomialRing", seed=None, noise_std: float = 3.2):
+        self.ring = ring
+        self.seed = seed if seed is not None else new_seed()
+        self.noise_std = float(noise_std)
+
+    def secret_key(self, stream: int, kind: int = SAMPLE_TERNARY, device_out: bool = False):
+        """generate_secret_key (:150-196): TERNARY (default), GAUSSIAN, BINARY or UNIFORM coefficients."""
+        return sample(self.ring, kind, self.seed, stream, self.ring.degree, self.noise_std, device_out=device_out)
+
+    def public_key(self, sk, stream: int, out=None):
+        """generate_public_key (:218-246) -> [2, n] = (a, a (*) s + e)."""
+        r = self.ring
+        sk = _as_u64(sk)
+        out = _empty(sk, (2, r.degree)) if out is None else out
+        bs, bo = _Buf(sk), _Buf(out, True)
+        w = _where(bs, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_public_key_generate(r._h, bs.ptr, _seed_arr(self.seed), stream, self.noise_std, bo.ptr, w))
+        return out
+
+    def eval_key(self, sk, base_log: int, level: int, stream: int, out=None):
+        """generate_eval_key (:252-333) -> rlk [level, 2, n] (KeySwitchKey pairs (a_l, b_l))."""
+        r = self.ring
+        sk = _as_u64(sk)
+        out = _empty(sk, (level, 2, r.degree)) if out is None else out
+        bs, bo = _Buf(sk), _Buf(out, True)
+        w = _where(bs, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_eval_key_generate(r._h, bs.ptr, base_log, level, _seed_arr(self.seed), stream,
+                                           self.noise_std, bo.ptr, w))
+        return out
+
+    def ggsw(self, values, sk, k: int, base_log: int, level: int, stream: int, out=None):
+        """encrypt_ggsw (bootstrap_engine.cpp:268-306) of int64 values ->
+        [count, (k+1) level, k+1, n] coefficient form."""
+        r = self.ring
+        if _is_tensor(values):
+            vals = values.to(torch.int64).contiguous()
+        else:
+            vals = np.ascontiguousarray(np.asarray(values, dtype=np.int64)).view(np.uint64)
+        sk = _as_u64(sk)
+        cnt = int(vals.numel() if _is_tensor(vals) else vals.size)
+        out = _empty(sk, (cnt, (k + 1) * level, k + 1, r.degree)) if out is None else out
+        bv, bs, bo = _Buf(vals), _Buf(sk), _Buf(out, True)
+        w = _where(bv, bs, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_ggsw_encrypt_batch(r._h, k, base_log, level, bv.ptr, cnt, bs.ptr, _seed_arr(self.seed),
+                                            stream, self.noise_std, bo.ptr, w))
+        return out
+
+    def key_switch_key(self, glwe_sk, lwe_sk, base_log: int, level: int, stream: int, std_dev: float = 0.0):
+        """generate_key_switch_key (:367-420) -> (ksk_a [n_in level, dim], ksk_b [n_in level])."""
+        r = self.ring
+        g = _as_u64(glwe_sk)
+        if _is_tensor(lwe_sk):
+            ls = lwe_sk.to(torch.int64).contiguous()
+        else:
+            ls = np.ascontiguousarray(np.asarray(lwe_sk, dtype=np.int64)).view(np.uint64)
+        n_in = int(g.numel() if _is_tensor(g) else g.size)
+        dim = int(ls.numel() if _is_tensor(ls) else ls.size)
+        ka, kb = _empty(g, (n_in * level, dim)), _empty(g, (n_in * level,))
+        bg, bl, ba, bb = _Buf(g), _Buf(ls), _Buf(ka, True), _Buf(kb, True)
+        w = _where(bg, bl, ba, bb)
+        r._bind_stream(w)
+        _check(lib().fhe_ksk_generate(r._h, base_log, level, bg.ptr, n_in, bl.ptr, dim, _seed_arr(self.seed), stream,
+                                      float(std_dev), ba.ptr, bb.ptr, w))
+        return ka, kb
+
+
+def lwe_decrypt(q: int, t: int, sk, lwe_a, lwe_b, device: int = 0):
+    """LWE decryption (fhe_lwe_decrypt_batch): (values [batch], phase [batch])."""
+    if _is_tensor(lwe_a):
+        skv = sk.to(torch.int64).contiguous() if _is_tensor(sk) else torch.as_tensor(np.asarray(sk, dtype=np.int64),
+                                                                                      device=lwe_a.device)
+    else:
+        skv = np.ascontiguousarray(np.asarray(sk, dtype=np.int64)).view(np.uint64)
+    a, b = _as_u64(lwe_a), _as_u64(lwe_b)
+    batch = int(b.numel() if _is_tensor(b) else b.size)
+    dim = int(skv.numel() if _is_tensor(skv) else skv.size)
+    vals, ph = _empty(b, (batch,)), _empty(b, (batch,))
+    bs, ba, bb, bv, bp = _Buf(skv), _Buf(a), _Buf(b), _Buf(vals, True), _Buf(ph, True)
+    w = _where(bs, ba, bb, bv, bp)
+    stream = _stream_ptr(bv.device) if w == FHE_DEVICE else None
+    _check(lib().fhe_lwe_decrypt_batch(q, t, bs.ptr, dim, ba.ptr, bb.ptr, bv.ptr, bp.ptr, batch, w, device, stream))
+    return vals, ph
+
+
 class DecryptionResult:
     """Batched DecryptionResult (encryption.h): decoded slot values
     [..., n] (slot 0 is decrypt_value's result), the reference's noise budget
@@ -718,6 +858,23 @@ class EncryptionEngine:
         w = _where(bk, bv, bu, b1, b2, bo)
         r._bind_stream(w)
         _check(lib().fhe_encrypt_batch(r._h, self.t, bk.ptr, bv.ptr, bu.ptr, b1.ptr, b2.ptr, bo.ptr, nb, w))
+        return out
+
+    def encrypt_sampled(self, values, pk: PublicKey, seed, stream: int, noise_std: float = 3.2, batch=None,
+                        out=None):
+        """encrypt_internal (:171-205) with u (ternary), e1, e2 (error) drawn
+        on the device from the seeded stream (streams stream .. stream + 2)."""
+        r = self.ring
+        v = _as_u64(values)
+        nb = batch if batch is not None else (r._batch(v) if (v.shape[-1] if len(v.shape) else 0) == r.degree else 1)
+        vals = self._slots(values, nb)
+        if out is None:
+            out = _empty(pk.prep, (nb, 2, r.degree))
+        bk, bv, bo = _Buf(pk.prep), _Buf(vals), _Buf(out, True)
+        w = _where(bk, bv, bo)
+        r._bind_stream(w)
+        _check(lib().fhe_encrypt_sampled_batch(r._h, self.t, bk.ptr, bv.ptr, _seed_arr(seed), stream,
+                                               float(noise_std), bo.ptr, nb, w))
         return out
 
     def decrypt(self, ct, sk: SecretKey, is_ntt: bool = False, with_phase: bool = False):

@@ -301,12 +301,13 @@ class GpuFHEEngine {
   dispose() { this.ring = null; this.ctx = null; }
 }
 
-/** createEngine (src/index.ts:108): a preset name or custom parameters. */
-async function createEngine(params, options) {
-  const p = typeof params === 'string' ? PRESETS[params] : params;
-  if (!p) throw new RangeError(`Unknown parameter preset: ${params}`);
-  return new GpuFHEEngine(p, options);
-}
+/* createEngine (src/index.ts:108, api/fhe-engine.ts:464-476): a preset name
+ * or custom parameters -> the FHEEngine surface with device-resident
+ * handles (lib/engine.js).  GpuFHEEngine above is the array-level engine
+ * (raw BigUint64Array ciphertexts, caller-supplied randomness) kept for
+ * batch callers and the golden tests. */
+const engine = require('./engine');
+const { createEngine, FHEEngineImpl } = engine.makeEngineClass(native);
 
 module.exports = {
   initialize: native.initialize,
@@ -314,11 +315,20 @@ module.exports = {
   version: native.version,
   ModularArithmetic: native.ModularArithmetic,
   NttContext: native.NttContext,
+  DeviceBuffer: native.DeviceBuffer,
   modmulBatch: native.modmulBatch,
   mlMontgomeryMulBatch: native.mlMontgomeryMulBatch,
   PolynomialEngine,
   GpuFHEEngine,
+  FHEEngineImpl,
   createEngine,
+  createFHEEngine: createEngine,
+  createParameterSet: engine.createParameterSet,
+  getAvailablePresets: engine.getAvailablePresets,
+  calculateDerivedParameters: engine.calculateDerivedParameters,
+  NTT_PRIMES: engine.NTT_PRIMES,
+  FHEError: engine.FHEError,
+  FHEErrorCode: engine.FHEErrorCode,
   PRESETS,
   sampling: { uniformMod, ternary, gaussian },
 };

@@ -98,6 +98,16 @@ def lib():
         L.oracle_mt19937_64_raw.argtypes = [C.c_uint64, u64p, C.c_size_t]
         L.oracle_splitmix_fill.argtypes = [C.c_uint64, C.c_uint64, u64p, C.c_size_t, C.c_size_t]
         L.oracle_batch_threaded.argtypes = [C.c_void_p, C.c_int, u64p, u64p, u64p, C.c_size_t, C.c_int]
+        i64p = C.POINTER(C.c_int64)
+        L.oracle_sample.argtypes = [C.c_int, u64p, C.c_uint64, C.c_uint64, C.c_double, u64p, C.c_size_t]
+        L.oracle_public_key_generate.argtypes = [C.c_void_p, u64p, u64p, C.c_uint64, C.c_double, u64p]
+        L.oracle_eval_key_generate.argtypes = [C.c_void_p, u64p, C.c_uint32, C.c_uint32, u64p, C.c_uint64, C.c_double,
+                                               u64p]
+        L.oracle_ggsw_encrypt.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, i64p, C.c_size_t, u64p,
+                                          u64p, C.c_uint64, C.c_double, u64p]
+        L.oracle_ksk_generate.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, u64p, C.c_uint32, i64p, C.c_uint32,
+                                          u64p, C.c_uint64, C.c_double, u64p, u64p]
+        L.oracle_lwe_decrypt.argtypes = [C.c_uint64, C.c_uint64, i64p, C.c_uint32, u64p, C.c_uint64, u64p, u64p]
         _lib = L
     return _lib
 
@@ -297,6 +307,51 @@ def splitmix_fill(seed, q, count, offset=0):
     return out
 
 
+# ---------------------------------------------------------------- key material / randomness
+SAMPLE_UNIFORM, SAMPLE_TERNARY, SAMPLE_GAUSSIAN, SAMPLE_BINARY, SAMPLE_RAW = range(5)
+
+
+def _seed(seed):
+    s = np.ascontiguousarray(seed, dtype=np.uint64)
+    assert s.size == 4
+    return s
+
+
+def _i64p(a):
+    assert a.dtype == np.int64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def sample(kind, seed, stream, q, count, std_dev=0.0):
+    """SecureRandom draws (key_manager.cpp:53-115) over the seeded ChaCha20 stream."""
+    s = _seed(seed)
+    out = np.empty(count, dtype=np.uint64)
+    lib().oracle_sample(kind, _p(s), stream, q, std_dev, _p(out), count)
+    return out
+
+
+def ksk_generate(q, base_log, level, glwe_sk, lwe_sk, seed, stream, std_dev=0.0):
+    """generate_key_switch_key (bootstrap_engine.cpp:367-420) -> (ksk_a [n_in*L][dim], ksk_b [n_in*L])."""
+    g = np.ascontiguousarray(glwe_sk, dtype=np.uint64)
+    ls = np.ascontiguousarray(lwe_sk, dtype=np.int64)
+    s = _seed(seed)
+    ka = np.empty((g.size * level, ls.size), dtype=np.uint64)
+    kb = np.empty(g.size * level, dtype=np.uint64)
+    lib().oracle_ksk_generate(q, base_log, level, _p(g), g.size, _i64p(ls), ls.size, _p(s), stream, std_dev,
+                              _p(ka), _p(kb))
+    return ka, kb
+
+
+def lwe_decrypt(q, t, sk, a, b):
+    """phase = b - <a, s> mod q; value = round(phase t / q) % t -> (value, phase)."""
+    sk = np.ascontiguousarray(sk, dtype=np.int64)
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    v = np.zeros(1, dtype=np.uint64)
+    ph = np.zeros(1, dtype=np.uint64)
+    lib().oracle_lwe_decrypt(q, t, _i64p(sk), sk.size, _p(a), int(b), _p(v), _p(ph))
+    return int(v[0]), int(ph[0])
+
+
 class NTT:
     """Restated NTTProcessor(degree, modulus) (ntt_processor.cpp:134-160)."""
 
@@ -422,6 +477,27 @@ class NTT:
         lib().oracle_bootstrap(self._h, k, base_log, level, lwe_a.size, _p(lwe_a), int(lwe_b), lwe_q, _p(bsk),
                                _p(test_poly), ks_base_log, ks_level, out_dim, _p(ksk_a), _p(ksk_b), _p(oa), _p(ob))
         return oa, int(ob[0])
+
+    # ---- key generation over the seeded stream (key_manager.cpp, bootstrap_engine.cpp)
+    def public_key_generate(self, sk, seed, stream, std_dev):
+        sk = np.ascontiguousarray(sk, dtype=np.uint64)
+        pk = np.empty((2, self.n), dtype=np.uint64)
+        lib().oracle_public_key_generate(self._h, _p(sk), _p(_seed(seed)), stream, std_dev, _p(pk))
+        return pk
+
+    def eval_key_generate(self, sk, base_log, level, seed, stream, std_dev):
+        sk = np.ascontiguousarray(sk, dtype=np.uint64)
+        rlk = np.empty((level, 2, self.n), dtype=np.uint64)
+        lib().oracle_eval_key_generate(self._h, _p(sk), base_log, level, _p(_seed(seed)), stream, std_dev, _p(rlk))
+        return rlk
+
+    def ggsw_encrypt(self, k, base_log, level, values, sk, seed, stream, std_dev):
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        sk = np.ascontiguousarray(sk, dtype=np.uint64)
+        out = np.empty((v.size, (k + 1) * level, k + 1, self.n), dtype=np.uint64)
+        lib().oracle_ggsw_encrypt(self._h, k, base_log, level, _i64p(v), v.size, _p(sk), _p(_seed(seed)), stream,
+                                  std_dev, _p(out))
+        return out
 
     def batch_threaded(self, op, a, b=None, c=None, threads=1):
         """op: 0 fwd (in place), 1 inv (in place), 2 polymul, 3 fwd+mul."""

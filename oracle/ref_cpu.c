@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <math.h>
 
 typedef unsigned __int128 u128;
 typedef uint64_t u64;
@@ -763,6 +764,185 @@ void oracle_bootstrap(const oracle_ntt *t, u32 k, u32 base_log, u32 level, u32 l
     oracle_sample_extract(t->q, k, n, acc, ea, &eb);
     oracle_key_switch(t->q, ks_base_log, ks_level, k * n, out_dim, ksk_a, ksk_b, ea, eb, out_a, out_b);
     free(acc); free(ea);
+}
+
+/* ------------------------------------------------------------------------
+ * Key material and encryption randomness (key_manager.cpp, bootstrap_engine.cpp)
+ * SecureRandom's draws (key_manager.cpp:53-115) are restated over the
+ * backend's seeded ChaCha20 stream (include/fhe_gpu.h, FHE_SAMPLE_*): RFC
+ * 8439 block function, key = seed[4] as 8 little-endian words, 64-bit block
+ * counter (words 12-13), 64-bit nonce = stream (words 14-15); element i of
+ * a stream of `count` draws from blocks i, i + count, i + 2 count, ...
+ * (8 u64 words per block).  The key formulas follow the reference lines
+ * cited at each function, with the reference's u64 / int64 wrap-around.
+ * ------------------------------------------------------------------------ */
+static u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
+#define CC_QR(a, b, c, d) \
+    a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12); \
+    a += b; d ^= a; d = rotl32(d, 8);  c += d; b ^= c; b = rotl32(b, 7);
+void oracle_chacha_block(const u64 seed[4], u64 counter, u64 nonce, u64 o[8]) {
+    u32 in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 4; ++i) { in[4 + 2 * i] = (u32)seed[i]; in[5 + 2 * i] = (u32)(seed[i] >> 32); }
+    in[12] = (u32)counter; in[13] = (u32)(counter >> 32); in[14] = (u32)nonce; in[15] = (u32)(nonce >> 32);
+    u32 x[16];
+    memcpy(x, in, sizeof x);
+    for (int r = 0; r < 10; ++r) {
+        CC_QR(x[0], x[4], x[8], x[12]) CC_QR(x[1], x[5], x[9], x[13])
+        CC_QR(x[2], x[6], x[10], x[14]) CC_QR(x[3], x[7], x[11], x[15])
+        CC_QR(x[0], x[5], x[10], x[15]) CC_QR(x[1], x[6], x[11], x[12])
+        CC_QR(x[2], x[7], x[8], x[13]) CC_QR(x[3], x[4], x[9], x[14])
+    }
+    for (int i = 0; i < 8; ++i) o[i] = (u64)(x[2 * i] + in[2 * i]) | ((u64)(x[2 * i + 1] + in[2 * i + 1]) << 32);
+}
+#undef CC_QR
+typedef struct { const u64 *seed; u64 nonce, idx, count, blk; int pos; u64 buf[8]; } draws_t;
+static u64 dr_next(draws_t *d) {
+    if (d->pos == 8) { oracle_chacha_block(d->seed, d->idx + d->blk * d->count, d->nonce, d->buf); d->blk++; d->pos = 0; }
+    return d->buf[d->pos++];
+}
+static u64 dr_range(draws_t *d, u64 max) { /* random_u64_range (:60-71) */
+    if (max == 0) return 0;
+    const u64 thr = (0ULL - max) % max;
+    u64 r;
+    do r = dr_next(d); while (r < thr);
+    return r % max;
+}
+static double dr_unit(draws_t *d) { return (double)(dr_next(d) >> 11) * 0x1.0p-53; }
+/* kind: 0 uniform mod q, 1 ternary, 2 gaussian(std), 3 binary, 4 raw */
+void oracle_sample(int kind, const u64 seed[4], u64 stream, u64 q, double std_dev, u64 *out, size_t count) {
+    for (size_t i = 0; i < count; ++i) {
+        draws_t d = {seed, stream, (u64)i, (u64)count, 0, 8, {0}};
+        u64 v;
+        switch (kind) {
+        case 0: v = dr_range(&d, q); break;
+        case 1: { const u64 r = dr_range(&d, 3); v = r == 0 ? q - 1 : (r == 1 ? 0 : 1); break; } /* :73-83 */
+        case 2: { /* sample_gaussian (:85-110) */
+            double u1 = dr_unit(&d);
+            const double u2 = dr_unit(&d);
+            while (u1 == 0.0) u1 = dr_unit(&d);
+            const double z = sqrt(-2.0 * log(u1)) * cos(2.0 * 3.14159265358979323846 * u2);
+            int64_t iv = (int64_t)round(z * std_dev);
+            if (iv < 0) { iv = (int64_t)q + iv; while (iv < 0) iv += (int64_t)q; }
+            v = (u64)iv % q;
+            break;
+        }
+        case 3: v = dr_next(&d) & 1; break;
+        default: v = dr_next(&d);
+        }
+        out[i] = v;
+    }
+}
+/* PolynomialRing product as the key code spells it: from_ntt(to_ntt(a) . to_ntt(b)) */
+static void ring_product(const oracle_ntt *t, const u64 *a, const u64 *b, u64 *out) {
+    const u32 n = t->n;
+    u64 *x = (u64 *)malloc(8 * (size_t)n * 2), *y = x + n;
+    memcpy(x, a, 8 * (size_t)n); memcpy(y, b, 8 * (size_t)n);
+    oracle_ntt_forward(t, x); oracle_ntt_forward(t, y);
+    oracle_pointwise(t->q, x, y, out, n);
+    oracle_ntt_inverse(t, out);
+    free(x);
+}
+/* generate_public_key (key_manager.cpp:218-246): pk [2][n] = (a, a*s + e);
+ * a uniform (stream), e gaussian (stream + 1) */
+void oracle_public_key_generate(const oracle_ntt *t, const u64 *sk, const u64 seed[4], u64 stream, double std_dev,
+                                u64 *pk) {
+    const u32 n = t->n;
+    u64 *e = (u64 *)malloc(8 * (size_t)n);
+    oracle_sample(0, seed, stream, t->q, 0, pk, n);
+    oracle_sample(2, seed, stream + 1, t->q, std_dev, e, n);
+    ring_product(t, pk, sk, pk + n);
+    oracle_poly_add(t->q, pk + n, e, pk + n, n);
+    free(e);
+}
+/* generate_eval_key (:252-333): s2 = s*s; level l: a uniform (stream + 2l),
+ * e gaussian (stream + 2l + 1), b = a*s + e + multiply_scalar(s2, power),
+ * power = (power * base) % q with the u64 product */
+void oracle_eval_key_generate(const oracle_ntt *t, const u64 *sk, u32 base_log, u32 level, const u64 seed[4],
+                              u64 stream, double std_dev, u64 *rlk) {
+    const u32 n = t->n; const u64 q = t->q;
+    u64 *w = (u64 *)malloc(8 * (size_t)n * 3), *s2 = w, *e = w + n, *sc = w + 2 * n;
+    ring_product(t, sk, sk, s2);
+    const u64 base = 1ULL << base_log;
+    u64 power = 1;
+    for (u32 l = 0; l < level; ++l) {
+        u64 *a = rlk + (size_t)2 * l * n, *b = a + n;
+        oracle_sample(0, seed, stream + 2 * l, q, 0, a, n);
+        oracle_sample(2, seed, stream + 2 * l + 1, q, std_dev, e, n);
+        ring_product(t, a, sk, b);
+        oracle_poly_add(q, b, e, b, n);
+        oracle_poly_mul_scalar(q, s2, power, sc, n);
+        oracle_poly_add(q, b, sc, b, n);
+        power = (power * base) % q;
+    }
+    free(w);
+}
+/* encrypt_ggsw (bootstrap_engine.cpp:268-306) for count values: out
+ * [count][(k+1)L][k+1][n].  Row r = row*L + l of value c is
+ * encrypt_glwe_zero (:190-227): masks uniform (stream, element
+ * ((c (k+1)L + r) k + i) n + j), error (stream + 1, element (c (k+1)L + r) n
+ * + j), body = 0 + sum_i mask_i * s (mod_add) + e; then the gadget
+ * (|v| q) >> ((l+1) B) (negated mod q for v < 0) added (% q) to coefficient
+ * 0 of mask[row] (row < k) or the body.  Shift counts mod 64. */
+void oracle_ggsw_encrypt(const oracle_ntt *t, u32 k, u32 base_log, u32 level, const int64_t *values, size_t count,
+                         const u64 *sk, const u64 seed[4], u64 stream, double std_dev, u64 *out) {
+    const u32 n = t->n; const u64 q = t->q;
+    const size_t rows = count * (k + 1) * level;
+    u64 *masks = (u64 *)malloc(8 * rows * k * n), *err = (u64 *)malloc(8 * rows * n);
+    u64 *prod = (u64 *)malloc(8 * (size_t)n);
+    oracle_sample(0, seed, stream, q, 0, masks, rows * k * n);
+    oracle_sample(2, seed, stream + 1, q, std_dev, err, rows * n);
+    for (size_t r = 0; r < rows; ++r) {
+        const size_t c = r / ((k + 1) * level);
+        const u32 rr = (u32)(r % ((k + 1) * level)), grp = rr / level, l = rr % level;
+        u64 *o = out + r * (k + 1) * n, *body = o + (size_t)k * n;
+        memset(body, 0, 8 * (size_t)n);
+        for (u32 i = 0; i < k; ++i) {
+            memcpy(o + (size_t)i * n, masks + (r * k + i) * n, 8 * (size_t)n);
+            ring_product(t, o + (size_t)i * n, sk, prod);
+            oracle_poly_add(q, body, prod, body, n);
+        }
+        oracle_poly_add(q, body, err + r * n, body, n);
+        const int64_t v = values[c];
+        const u64 av = v < 0 ? (u64)0 - (u64)v : (u64)v;
+        u64 g = (av * q) >> (((l + 1) * base_log) & 63);
+        if (v < 0) g = (q - g) % q;
+        if (grp < k) o[(size_t)grp * n] = (o[(size_t)grp * n] + g) % q;
+        else body[0] = (body[0] + g) % q;
+    }
+    free(masks); free(err); free(prod);
+}
+/* generate_key_switch_key (:367-420): entry e = i L + l: a_e uniform
+ * (stream, element e*lwe_dim + j), error (stream + 1, element e; std_dev 0
+ * selects 3.2), b_e = ((u64)((ip + err) % (int64)q) + gadget) % q */
+void oracle_ksk_generate(u64 q, u32 base_log, u32 level, const u64 *glwe_sk, u32 n_in, const int64_t *lwe_sk,
+                         u32 lwe_dim, const u64 seed[4], u64 stream, double std_dev, u64 *ksk_a, u64 *ksk_b) {
+    const size_t entries = (size_t)n_in * level;
+    u64 *err = (u64 *)malloc(8 * (entries ? entries : 1));
+    oracle_sample(0, seed, stream, q, 0, ksk_a, entries * lwe_dim);
+    oracle_sample(2, seed, stream + 1, q, std_dev > 0 ? std_dev : 3.2, err, entries);
+    for (size_t e = 0; e < entries; ++e) {
+        const u32 i = (u32)(e / level), l = (u32)(e % level);
+        u64 ip = 0; /* int64 accumulation, wrapping */
+        for (u32 j = 0; j < lwe_dim; ++j) ip += ksk_a[e * lwe_dim + j] * (u64)lwe_sk[j];
+        int64_t ev = (int64_t)err[e];
+        if (ev > (int64_t)(q / 2)) ev -= (int64_t)q;
+        const u64 gadget = (glwe_sk[i] * q) >> (((l + 1) * base_log) & 63);
+        const int64_t sm = (int64_t)(ip + (u64)ev);
+        ksk_b[e] = ((u64)(sm % (int64_t)q) + gadget) % q;
+    }
+    free(err);
+}
+/* LWE decryption: phase = b - sum_j a_j s_j mod q, value = round(phase t / q) % t */
+void oracle_lwe_decrypt(u64 q, u64 t, const int64_t *sk, u32 dim, const u64 *a, u64 b, u64 *value, u64 *phase) {
+    u64 s = 0;
+    for (u32 j = 0; j < dim; ++j) {
+        const u64 mag = (u64)(sk[j] < 0 ? -(u128)sk[j] : (u128)sk[j]) % q;
+        const u64 kq = sk[j] < 0 && mag ? q - mag : mag;
+        s = (u64)(((u128)s + (u64)((u128)(a[j] % q) * kq % q)) % q);
+    }
+    const u64 p = (b % q + q - s) % q;
+    if (phase) *phase = p;
+    if (value) *value = (u64)(((u128)p * ee_t(t) + q / 2) / q) % ee_t(t);
 }
 
 /* ------------------------------------------------------------------------

@@ -269,10 +269,79 @@ def engine():
     return out
 
 
+ENGINE_SEED = bytes(range(32))  # createEngine(params, { seed }) of tests/js/engine_test.js
+
+
+def _seed_words(b):
+    return [int(x) for x in np.frombuffer(b, dtype=np.uint64)]
+
+
+def _identity_test_poly(n, q, t):
+    """init_default_test_poly (bootstrap_engine.cpp:57-77)"""
+    delta = q // t
+    return np.array([((((i * t) // (2 * n)) * delta) & ((1 << 64) - 1)) % q for i in range(n)], dtype=np.uint64)
+
+
+def fhe_engine():
+    """The FHEEngine surface flows of tests/js/engine_test.js, regenerated with
+    the oracle's restatement of the seeded ChaCha20 sampler (oracle_sample)
+    and the key / encryption / ciphertext restatements.  Stream ids follow
+    lib/engine.js: a counter from 1, secret key 1 stream, public key 2,
+    encrypt 3, eval key 2 per level, bootstrap key 1 + 2 + 2."""
+    seed = _seed_words(ENGINE_SEED)
+    out = []
+    # bfv-128-simd: keys -> encryptPacked x2 -> multiply -> generateEvalKey -> relinearize -> decrypt
+    n, q, t, bl, lv, std = 8192, 1152921504606584833, 65537, 60, 2, 3.2
+    o = oracle.NTT(n, q)
+    sk = oracle.sample(1, seed, 1, q, n)
+    pk = o.public_key_generate(sk, seed, 2, std)
+    vals = [oracle.splitmix_fill(44 + j, t, n) for j in range(2)]
+    cts = []
+    for j in range(2):
+        s0 = 4 + 3 * j
+        cts.append(o.encrypt(t, pk, vals[j], oracle.sample(1, seed, s0, q, n),
+                             oracle.sample(2, seed, s0 + 1, q, n, std), oracle.sample(2, seed, s0 + 2, q, n, std)))
+    ct3 = o.ct_multiply(cts[0], cts[1])
+    rlk = o.eval_key_generate(sk, bl, lv, seed, 10, std)
+    rel = o.relinearize(bl, lv, ct3, rlk)
+    dv, _, mx = o.decrypt(t, sk, rel)
+    dv0, _, mx0 = o.decrypt(t, sk, cts[0])
+    added = oracle.poly_add(q, cts[0].ravel(), cts[1].ravel()).reshape(2, n)
+    dva, _, mxa = o.decrypt(t, sk, added)
+    out.append({"op": "engine_flow", "preset": "bfv-128-simd", "n": n, "q": q, "t": t, "base_log": bl, "level": lv,
+                "values_seeds": [44, 45], "sha_ct0": sha(cts[0]), "sha_ct1": sha(cts[1]), "sha_ct3": sha(ct3),
+                "sha_relin": sha(rel), "sha_dec": sha(dv), "max_noise": mx, "sha_dec_ct0": sha(dv0),
+                "max_noise_ct0": mx0, "sha_add": sha(added), "sha_dec_add": sha(dva), "max_noise_add": mxa})
+    # tfhe-128-balanced: keys -> generateBootstrapKey -> encryptValue -> bootstrap -> decrypt (LWE)
+    n, q, t, bl, lv, dim, std = 2048, 1125899906826241, 8, 15, 2, 830, 2.9e-11
+    o = oracle.NTT(n, q)
+    sk = oracle.sample(1, seed, 1, q, n)
+    pk = o.public_key_generate(sk, seed, 2, std)
+    lwe_sk = oracle.sample(3, seed, 4, q, dim).astype(np.int64)
+    bsk = o.ggsw_encrypt(1, bl, lv, lwe_sk, sk, seed, 5, std)
+    ksk_a, ksk_b = oracle.ksk_generate(q, bl, lv, sk, lwe_sk, seed, 7, std)
+    value = 3
+    slots = np.zeros(n, dtype=np.uint64)
+    slots[0] = value
+    ct = o.encrypt(t, pk, slots, oracle.sample(1, seed, 9, q, n), oracle.sample(2, seed, 10, q, n, std),
+                   oracle.sample(2, seed, 11, q, n, std))
+    glwe = np.stack([ct[1], ct[0]])
+    ea, eb = oracle.sample_extract(q, glwe)
+    la, lb = oracle.key_switch(q, bl, lv, ksk_a, ksk_b, ea, eb)
+    oa, ob = o.bootstrap(1, bl, lv, la, lb, q, bsk, _identity_test_poly(n, q, t), bl, lv, ksk_a, ksk_b)
+    lwe_out = np.concatenate([oa, np.array([ob], dtype=np.uint64)])
+    v, ph = oracle.lwe_decrypt(q, t, lwe_sk, oa, ob)
+    out.append({"op": "tfhe_flow", "preset": "tfhe-128-balanced", "n": n, "q": q, "t": t, "dim": dim, "value": value,
+                "sha_bsk": sha(bsk), "sha_ksk_a": sha(ksk_a), "sha_ksk_b": sha(ksk_b), "sha_ct": sha(ct),
+                "sha_keyswitched": sha(np.concatenate([la, np.array([lb], dtype=np.uint64)])),
+                "sha_bootstrapped": sha(lwe_out), "decrypted": v, "phase": ph})
+    return out
+
+
 GENERATORS = {
     "reference_kat.json": reference_kat, "ntt_small.json": ntt_small, "ntt_large.json": ntt_large,
     "modmul.json": modmul, "multi_limb.json": multi_limb, "extprod.json": extprod, "negacyclic.json": negacyclic,
-    "cipher.json": cipher, "engine.json": engine,
+    "cipher.json": cipher, "engine.json": engine, "fhe_engine.json": fhe_engine,
 }
 
 if __name__ == "__main__":

@@ -120,7 +120,7 @@ if (mode === 'cpu') {
     for (const c of goldenBig('cipher.json')) {
       if (c.op === 'blind_rotate') continue;
       const custom = { polyDegree: c.n, moduli: [BigInt(c.q)], decompBaseLog: c.base_log || 4 };
-      pending.push(fhe.createEngine(custom).then(async (eng) => {
+      pending.push(Promise.resolve(new fhe.GpuFHEEngine(custom)).then(async (eng) => {
         const got = c.op === 'ct_multiply' ? await eng.multiply(U(c.ct1), U(c.ct2))
           : await eng.relinearize(U(c.ct3), U(c.rlk), c.base_log);
         assert.deepStrictEqual(Array.from(got), c.out.map(BigInt), `${c.op} n=${c.n}`);
@@ -166,9 +166,9 @@ if (mode === 'cpu') {
     }
     asyncTests.push(Promise.all(pending));
   });
-  test("createEngine('bfv-128-simd'): encrypt -> multiply -> relinearize -> decrypt vs golden", () => {
+  test("GpuFHEEngine (array level) bfv-128-simd: encrypt -> multiply -> relinearize -> decrypt vs golden", () => {
     const c = goldenBig('engine.json').find((x) => x.op === 'bfv_flow');
-    asyncTests.push(fhe.createEngine(c.preset).then(async (eng) => {
+    asyncTests.push(Promise.resolve(new fhe.GpuFHEEngine(fhe.PRESETS[c.preset])).then(async (eng) => {
       const n = c.n, q = BigInt(c.q), S = c.seeds;
       assert.strictEqual(eng.getSlotCount(), n);
       assert.strictEqual(eng.q, q);
@@ -196,12 +196,15 @@ if (mode === 'cpu') {
       const d0 = await eng.decrypt(cts[0], sk);
       assert.strictEqual(sha(d0.values), c.sha_dec_ct0);
       assert.strictEqual(d0.maxNoise[0], BigInt(c.max_noise_ct0));
-      // the promise-returning forms run off the JS thread: the loop stays live
-      let ticks = 0;
-      const timer = setInterval(() => { ticks += 1; }, 0);
+      // the promise-returning forms run off the JS thread: the event loop
+      // turns (setImmediate callbacks run) while they are in flight
+      let ticks = 0, on = true;
+      const spin = () => { ticks += 1; if (on) setImmediate(spin); };
+      setImmediate(spin);
+      const before = ticks;
       await Promise.all([eng.multiply(cts[0], cts[1]), eng.multiply(cts[1], cts[0]), eng.decrypt(cts[1], sk)]);
-      clearInterval(timer);
-      assert.ok(ticks >= 0);
+      on = false;
+      assert.ok(ticks > before, 'event loop blocked while the async calls ran');
     }));
   });
   test('multi-device NttContext splits host batches', () => {

@@ -256,3 +256,78 @@ def test_external_product_equals_ntt_domain_accumulation(golden_dir):
             s = (s + oracle.pointwise(q, fd, t.forward(ggsw[r, j])).astype(object)) % q
         acc[j] = t.inverse(U(list(s)))
     assert [int(v) for v in np.concatenate(acc)] == c["out"]
+
+
+# ---------------------------------------------------------------- keygen randomness (oracle_sample)
+def test_chacha20_block_rfc8439_vector():
+    """RFC 8439 section 2.3.2 test vector through the oracle's block function
+    (key 00..1f; counter word 1 and nonce 00000009 0000004a 00000000 map to
+    the 64-bit counter / 64-bit nonce layout of include/fhe_gpu.h)."""
+    import ctypes as C
+
+    L = oracle.lib()
+    u64p = C.POINTER(C.c_uint64)
+    L.oracle_chacha_block.argtypes = [u64p, C.c_uint64, C.c_uint64, u64p]
+    seed = np.frombuffer(bytes(range(32)), dtype=np.uint64).copy()
+    out = np.zeros(8, dtype=np.uint64)
+    L.oracle_chacha_block(seed.ctypes.data_as(u64p), 1 | (0x09000000 << 32), 0x4A000000, out.ctypes.data_as(u64p))
+    assert out.tobytes().hex() == (
+        "10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+        "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+
+
+def test_sample_kinds_follow_secure_random():
+    """random_u64_range / sample_ternary / sample_binary (key_manager.cpp:60-114)
+    over the raw stream: every kind is a function of the same raw draws."""
+    seed, q = [5, 6, 7, 8], 97
+    raw = oracle.sample(4, seed, 3, 0, 1000)
+    binary = oracle.sample(3, seed, 3, q, 1000)
+    assert (binary == (raw & 1)).all()
+    thr = ((1 << 64) - q) % q
+    uni = oracle.sample(0, seed, 3, q, 1000)
+    ok = raw >= thr  # first draw accepted: value = raw % q
+    assert (uni[ok] == raw[ok] % q).all()
+    tern = oracle.sample(1, seed, 3, q, 1000)
+    t3 = raw % 3  # (2^64 - 3) % 3 == 1: raw 0 is rejected, never drawn here
+    assert (tern == np.where(t3 == 0, q - 1, np.where(t3 == 1, 0, 1))).all()
+    g = oracle.sample(2, seed, 3, 1 << 61, 200000, 3.2).astype(object)
+    s = np.array([int(v) - (1 << 61) if v > (1 << 60) else int(v) for v in g], dtype=np.int64)
+    assert abs(s.mean()) < 0.05 and abs(s.std() - 3.2) < 0.05
+    # element i of a stream does not depend on the other elements' rejections
+    assert (oracle.sample(0, seed, 3, q, 1000)[:10] == oracle.sample(0, seed, 3, q, 1000)[:10]).all()
+
+
+def test_keygen_restatements_are_consistent():
+    """pk / eval key / GGSW / KSK restatements satisfy their defining
+    equations under the restated transform product."""
+    n, q = 64, 7681
+    t = oracle.NTT(n, q)
+    seed = [1, 2, 3, 4]
+    sk = oracle.sample(1, seed, 1, q, n)
+    pk = t.public_key_generate(sk, seed, 2, 3.2)
+    e = oracle.sample(2, seed, 3, q, n, 3.2)
+    assert (oracle.poly_sub(q, pk[1], t.polymul(pk[0], sk)) == e).all()
+    rlk = t.eval_key_generate(sk, 4, 3, seed, 10, 3.2)
+    s2 = t.polymul(sk, sk)
+    for lv in range(3):
+        el = oracle.sample(2, seed, 10 + 2 * lv + 1, q, n, 3.2)
+        diff = oracle.poly_sub(q, oracle.poly_sub(q, rlk[lv, 1], t.polymul(rlk[lv, 0], sk)), el)
+        assert (diff == oracle.poly_mul_scalar(q, s2, (1 << (4 * lv)) % q)).all()
+    vals = np.array([1, -1, 0], dtype=np.int64)
+    g = t.ggsw_encrypt(1, 4, 2, vals, sk, seed, 20, 3.2)
+    masks = oracle.sample(0, seed, 20, q, 3 * 4 * n).reshape(3, 4, n)
+    for c in range(3):
+        for r in range(4):
+            m = masks[c, r].copy()
+            grp, lv = divmod(r, 2)
+            gad = (abs(int(vals[c])) * q) >> ((lv + 1) * 4)
+            if vals[c] < 0:
+                gad = (q - gad) % q
+            if grp == 0:
+                m[0] = (int(m[0]) + gad) % q
+            assert (g[c, r, 0] == m).all()
+    lwe = np.array([1, 0, 1, 1, 0], dtype=np.int64)
+    ka, kb = oracle.ksk_generate(q, 4, 2, sk[:8], lwe, seed, 40)
+    assert ka.shape == (16, 5) and kb.shape == (16,)
+    v, ph = oracle.lwe_decrypt(q, 4, lwe, ka[0], kb[0])
+    assert 0 <= ph < q and 0 <= v < 4
