@@ -46,6 +46,8 @@ def parse():
     ap.set_defaults(q62=True)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", default="compat", choices=["compat", "negacyclic"],
+                    help="transform of the --only profiling runs (the default run reports both)")
     ap.add_argument("--only", default="", help="run only this kernel (fwd_mul|polymul|fwd|inv) for profiling")
     ap.add_argument("--no-check", action="store_true", help="skip the oracle spot check (profiling runs)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-resident (FHE_HOST, PCIe) measurement")
@@ -139,8 +141,8 @@ def timed(dist, fn, steps, warmup):
     return max_over_ranks(dist, wall), max_over_ranks(dist, kernel_ms)
 
 
-def gpu_workload(fhe_gpu, n, q, batch, steps, warmup, dist, only="", check=True):
-    ring = fhe_gpu.PolynomialRing(n, q, device=torch.cuda.current_device())
+def gpu_workload(fhe_gpu, n, q, batch, steps, warmup, dist, only="", check=True, mode="compat"):
+    ring = fhe_gpu.PolynomialRing(n, q, mode=mode, device=torch.cuda.current_device())
     g = torch.Generator(device="cuda").manual_seed(1234 + int(os.environ.get("RANK", "0")))
     a = torch.randint(0, q, (batch, n), device="cuda", dtype=torch.int64, generator=g)
     b = torch.randint(0, q, (batch, n), device="cuda", dtype=torch.int64, generator=g)
@@ -159,6 +161,8 @@ def gpu_workload(fhe_gpu, n, q, batch, steps, warmup, dist, only="", check=True)
     # spot-check a few rows bit-exactly against the oracle (outside timing)
     if not check:
         res["parity_ok"] = "skipped"
+    elif mode == "negacyclic":
+        res["parity_ok"] = _spot_check_negacyclic(ring, a, b, out, n, q)
     else:
         res["parity_ok"] = _spot_check(ring, a, b, out, n, q, batch)
     del a, b, out
@@ -252,6 +256,129 @@ def _spot_check(ring, a, b, out, n, q, batch):
         return bool((got == t.fwd_mul(xa, xb)).all() and (got2 == t.polymul(xa, xb)).all())
     except Exception as e:  # pragma: no cover
         return f"unchecked: {e}"
+
+
+def _spot_check_negacyclic(ring, a, b, out, n, q):
+    """Negacyclic mode: the polymul rows are the ring product a*b mod (X^N+1)
+    (checked by the identity (a*b)(x) = a(x) b(x) at a random point x of the
+    field, for X^N = -1: x^N = -1 mod q picks x = psi^(2j+1)), and the
+    fwd_mul rows satisfy inv(fwd_mul(a, fwd(b))) == a*b."""
+    try:
+        rows = [0, a.shape[0] - 1]
+        xa, xb = a[rows].contiguous(), b[rows].contiguous()
+        c = ring.multiply(xa, xb).cpu().numpy().view(np.uint64)
+        psi = ring.primitive_root
+        x = pow(psi, 2 * 12345 + 1, q)  # a root of X^N + 1
+        ok = True
+        def ev(p):  # Horner evaluation of p at x mod q
+            acc = 0
+            for coef in reversed(p.tolist()):
+                acc = (acc * x + coef) % q
+            return acc
+
+        for r in range(len(rows)):
+            pa, pb = xa[r].cpu().numpy().view(np.uint64), xb[r].cpu().numpy().view(np.uint64)
+            ok &= (ev(pa) * ev(pb)) % q == ev(c[r])
+        fb = ring.forward_ntt(xb)
+        fm = ring.forward_ntt_mul(xa, fb)
+        ok &= bool((ring.inverse_ntt(fm).cpu().numpy().view(np.uint64) == c).all())
+        torch.cuda.synchronize()
+        return bool(ok)
+    except Exception as e:  # pragma: no cover
+        return f"unchecked: {e}"
+
+
+def negacyclic_workload(fhe_gpu, n, q, batch, steps, warmup, dist):
+    """north_star's forward negacyclic NTT (psi-twisted cyclic transform,
+    FHE_MODE_NEGACYCLIC) timed like the headline: C3 fwd NTT + modmul and C4
+    polymul, same batch, HIP-event kernel time, HBM fraction."""
+    r = gpu_workload(fhe_gpu, n, q, batch, steps, warmup, None if dist is None else dist, mode="negacyclic")
+    out = {"mode": "negacyclic", "n": n, "q": q, "batch": batch, "parity_ok": r["parity_ok"]}
+    for key in ("fwd_mul", "polymul"):
+        wall, kms = r[key]
+        ach = 24 * n * batch / (kms * 1e-3) / 1e9
+        out[key] = {"per_s": batch * steps / wall, "kernel_ms": kms, "achieved_GBs": ach,
+                    "frac": ach / HBM_PEAK_GBS, "bytes_per_unit": 24 * n}
+        tr = pmc_traffic(key, n, batch, q, mode="negacyclic")
+        if tr:
+            out[key]["traffic"], out[key]["traffic_source"] = tr
+            out[key]["traffic_over_algorithmic"] = tr[0] / (24 * n * batch)
+    return out
+
+
+def engine_chain(fhe_gpu, n=16384, q=1152921504606584833, t=65537, batch=256, reps=3):
+    """The FHEEngine chain encrypt -> multiply -> relinearize -> decrypt per
+    second at N=16384 (q = Q_60_1, t = 65537, base 2^20, 3 levels), on the
+    host-resident (FHE_HOST: every call stages host arrays through HBM, what
+    the N-API array calls do) and the device-resident (DeviceBuffer handles:
+    what lib/engine.js keeps) paths.  Never `value`."""
+    dev = torch.cuda.current_device()
+    ring = fhe_gpu.PolynomialRing(n, q, device=dev)
+    kg = fhe_gpu.KeyGenerator(ring, 2024, noise_std=3.2)
+    eng = fhe_gpu.EncryptionEngine(ring, t)
+    sk = kg.secret_key(1)
+    pk = fhe_gpu.PublicKey(ring, kg.public_key(sk, 2))
+    skp = fhe_gpu.SecretKey(ring, sk)
+    ek = fhe_gpu.EvaluationKey(ring, kg.eval_key(sk, 20, 3, 10), 20)
+    vals = np.random.default_rng(3).integers(0, t, size=(batch, n), dtype=np.uint64)
+
+    def chain(v, pkx, skx, ekx):
+        c1 = eng.encrypt_sampled(v, pkx, 7, 100, 3.2)
+        c2 = eng.encrypt_sampled(v, pkx, 7, 200, 3.2)
+        return eng.decrypt(eng.relinearize(eng.multiply(c1, c2), ekx), skx)
+
+    res = {"n": n, "q": q, "t": t, "batch": batch, "chain": "encrypt x2 -> multiply -> relinearize -> decrypt"}
+    chain(vals[:2], pk, skp, ek)  # warm-up
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        chain(vals, pk, skp, ek)
+        best = min(best or 1e9, time.perf_counter() - t0)
+    res["host_resident"] = {"per_s": batch / best, "ms": best * 1e3}
+    # device-resident: the keys and plaintext slots in HBM, outputs stay there
+    dv = torch.from_numpy(vals.view(np.int64)).to(f"cuda:{dev}")
+    pkd = fhe_gpu.PublicKey(ring, torch.from_numpy(pk.poly.view(np.int64)).to(f"cuda:{dev}"))
+    skd = fhe_gpu.SecretKey(ring, torch.from_numpy(sk.view(np.int64)).to(f"cuda:{dev}"))
+    ekd = fhe_gpu.EvaluationKey(ring, torch.from_numpy(kg.eval_key(sk, 20, 3, 10).view(np.int64)).to(f"cuda:{dev}"),
+                                20)
+    chain(dv[:2], pkd, skd, ekd)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        chain(dv, pkd, skd, ekd)
+        torch.cuda.synchronize()
+        best = min(best or 1e9, time.perf_counter() - t0)
+    res["device_resident"] = {"per_s": batch / best, "ms": best * 1e3}
+    del dv
+    torch.cuda.empty_cache()
+    return res
+
+
+def cpu_baseline_c2(n, q, seconds, threads):
+    """SURVEY.md 8(d) / BASELINE config 2 (N=4096, batch 1024, fwd + inv +
+    polymul, "1xMI355X vs CPU"): the oracle's restated NTTProcessor /
+    PolynomialRing on the host cores, each op in turn over contiguous chunks."""
+    import oracle
+
+    t = oracle.NTT(n, q)
+    B = max(threads * 4, 64)
+    a = oracle.splitmix_fill(11, q, B * n).reshape(B, n)
+    b = oracle.splitmix_fill(12, q, B * n).reshape(B, n)
+    c = np.empty_like(a)
+    out = {"n": n, "q": q, "cores": threads, "kind": "port"}
+    for name, op in (("fwd", 0), ("inv", 1), ("polymul", 2)):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            x = a.copy()
+            t.batch_threaded(op, x, b if op == 2 else None, c if op == 2 else None, threads=threads)
+            done += B
+            el = time.perf_counter() - t0
+            if el >= seconds / 3:
+                break
+        out[name] = {"per_s": done / el, "sample": f"{done} x {name}, {threads} threads, {el:.1f}s"}
+    return out
 
 
 def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
@@ -353,7 +480,7 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
 KERNEL_SYMBOL = {"fwd_mul": "k_ntt_fwd_mul", "polymul": "k_polymul", "fwd": "k_ntt_fwd", "inv": "k_ntt_inv"}
 
 
-def pmc_traffic(kernel, n, batch, q):
+def pmc_traffic(kernel, n, batch, q, mode="compat"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of the
     same workload (profiles/*/summary.json, tools/summarize_profile.py).
     Only summaries whose profiled kernel is the template this run launches
@@ -376,6 +503,7 @@ def pmc_traffic(kernel, n, batch, q):
             continue
         w = s.get("workload", {})
         if not (w.get("kernel") == kernel and w.get("n") == n and w.get("batch") == batch and w.get("q") == q
+                and w.get("mode", "compat") == mode
                 and "hbm_traffic_bytes_per_launch" in s and sym in s.get("kernel_name", "")):
             continue
         key = (s.get("generated", ""), f)
@@ -453,20 +581,39 @@ def main():
         if rank == 0:
             print(json.dumps({"cipher": c}), flush=True)
         return
-    r = gpu_workload(fhe_gpu, n, args.q, B, K, W, dist, args.only, check=not args.no_check)
+    if args.only == "engine":
+        if rank == 0:
+            print(json.dumps({"engine_chain": engine_chain(fhe_gpu)}), flush=True)
+        return
+    r = gpu_workload(fhe_gpu, n, args.q, B, K, W, dist, args.only, check=not args.no_check, mode=args.mode)
     if args.q62 and not args.only:
         r62 = gpu_workload(fhe_gpu, n, P62, B, max(3, K // 4), 1, dist)
+        ach62 = 24 * n * B / (r62["fwd_mul"][1] * 1e-3) / 1e9
+        achp62 = 24 * n * B / (r62["polymul"][1] * 1e-3) / 1e9
         extra["q62"] = {
             "q": P62,
             "ntt_fwd_mul_per_s": world * B * max(3, K // 4) / r62["fwd_mul"][0],
             "polymuls_per_s": world * B * max(3, K // 4) / r62["polymul"][0],
             "fwd_mul_kernel_ms": r62["fwd_mul"][1], "polymul_kernel_ms": r62["polymul"][1],
             "parity_ok": r62["parity_ok"],
+            "roofline": {"bound": "hbm", "achieved": ach62, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach62 / HBM_PEAK_GBS, "kernel": "fwd_mul"},
+            "polymul_roofline": {"achieved": achp62, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": achp62 / HBM_PEAK_GBS},
         }
+        for key, rl in (("fwd_mul", extra["q62"]["roofline"]), ("polymul", extra["q62"]["polymul_roofline"])):
+            tr = pmc_traffic(key, n, B, P62)
+            if tr:
+                rl["traffic"], rl["traffic_source"] = tr
+                rl["traffic_over_algorithmic"] = tr[0] / (24 * n * B)
+    if not args.only:
+        nk = max(3, K // 4)
+        extra["negacyclic"] = negacyclic_workload(fhe_gpu, n, args.q, B, nk, 1, dist)
     if args.cipher and not args.only:
         extra["cipher"] = cipher_workload(fhe_gpu, max(3, K // 4), 1, dist)
     if rank == 0 and not args.only and not args.no_host:
         extra["host_resident"] = host_resident(fhe_gpu, n, args.q)
+        extra["engine_chain"] = engine_chain(fhe_gpu)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -524,6 +671,12 @@ def main():
         # also one thread (the reference's sequential forward_ntt_batch)
         line["cpu_baseline_1thread"] = cpu_baseline(n, args.q, min(4.0, args.cpu_seconds), threads=1)
         line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        # BASELINE config 2 beside its GPU figures (cipher.c2)
+        c2cpu = cpu_baseline_c2(4096, args.q, min(9.0, args.cpu_seconds), line["cpu_baseline"]["cores"])
+        line["cpu_baseline_c2"] = c2cpu
+        g2 = line.get("cipher", {}).get("c2")
+        if g2:
+            line["c2_speedup_vs_cpu"] = {k: g2[k]["per_s"] / c2cpu[k]["per_s"] for k in ("fwd", "inv", "polymul")}
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -31,8 +31,11 @@ def main():
     out = {"source": src, "kernel_substr": ksub,
            "generated": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
     if "--workload" in sys.argv:
-        k, n, b, q = sys.argv[sys.argv.index("--workload") + 1].split(",")
+        parts = sys.argv[sys.argv.index("--workload") + 1].split(",")
+        k, n, b, q = parts[:4]
         out["workload"] = {"kernel": k, "n": int(n), "batch": int(b), "q": int(q)}
+        if len(parts) > 4:
+            out["workload"]["mode"] = parts[4]
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
