@@ -156,8 +156,16 @@ constexpr int eng_occ4() {
     return w < 4 ? w : 4;
 }
 
+// decrypt at 64-bit words and N = 256..2048 (several polynomials per
+// 256-thread workgroup): 2 waves per SIMD -- the decode epilogue beside a
+// 16-word u64 spectrum does not fit 128 VGPRs there
+template <int LOGN, typename W>
+constexpr int dec_occ() {
+    return (sizeof(W) == 8 && Geo<LOGN>::L >= 8 && Geo<LOGN>::L <= 11) ? 2 : eng_occ4<LOGN, W>();
+}
+
 template <int LOGN, typename W, bool NEGA, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (eng_occ4<LOGN, W>()))
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (dec_occ<LOGN, W>()))
 k_decrypt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * G::LW];
@@ -195,48 +203,37 @@ k_decrypt(EngArgs E, NttArgs<W> A) {
                 x = A.ar.red1q(A.ar.red2q(x + A.ar.mont((W)red_q(ct[2 * G::N + gi], q, mu), (W)E.key[G::N + gi])));
             v[e] = (W)subq(red_q(ct[gi], q, mu), (uint64_t)x, q);
         }
-        inv_poly_from_regs<LOGN, NEGA, kPfSingle, false>(lds, v, tau, phase, valid, A, A.ninv, A.untwist, 0, 0,
-                                                         final_fin);
     } else {
-        // pass 1: c0 - inv(fwd(c1) S)
-        fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, ct + G::N, valid, A);
+        // c0 - inv(fwd(c1) S) [- inv(fwd(c2) S^2)] == c0 - inv(fwd(c1) S [+ fwd(c2) S^2]):
+        // the inverse is linear over Z_q and the phase is taken canonical, so
+        // one inverse serves both components (bit-exact).  One forward
+        // instance in a runtime loop; the c1 product waits in this thread's
+        // own positions of the phase row (W words) while fwd(c2) runs.
+        W *stash = reinterpret_cast<W *>(phase);
+        for (int c = 1; c < E.comps; ++c) {
+            uint32_t tc = tau;
+            asm volatile("" : "+v"(tc));
+            fwd_poly<LOGN, NEGA, LAZY>(lds, v, tc, ct + (size_t)c * G::N, valid, A);
+            const bool last = c + 1 == E.comps;
 #pragma unroll
-        for (int e = 0; e < G::E; ++e)
-            v[e] = valid ? A.ar.mont(v[e], (W)E.key[gidx<LOGN, G::NP - 1>(tau, e)]) : W(0);
-        if constexpr (G::NP > 1) __syncthreads();
+            for (int e = 0; e < G::E; ++e) {
+                const uint32_t gi = gidx<LOGN, G::NP - 1>(tc, e);
+                W x = valid ? A.ar.mont(v[e], (W)E.key[(size_t)(c - 1) * G::N + gi]) : W(0);  // [0, 2q)
+                if (c == 2 && valid) x = A.ar.red2q(x + stash[gi]);
+                if (!last && valid) stash[gi] = x;
+                v[e] = x;
+            }
+            if constexpr (G::NP > 1) __syncthreads();  // exchange buffer reuse; stash reads before the final stores
+        }
+    }
+    {
         uint32_t tr = tau;
         asm volatile("" : "+v"(tr));
-        if (E.comps == 3) {
-            // the partial phase goes to this thread's own store positions
-            // of the phase row; pass 2 reads it back at the same positions
-            auto fin_part = [&](uint32_t gi, uint64_t x) -> uint64_t {
-                if (valid) phase[gi] = subq(red_q(ct[gi], q, mu), x, q);
-                return 0;
-            };
-            inv_poly_from_regs<LOGN, NEGA, kPfSingle, false>(lds, v, tr, phase, valid, A, A.ninv, A.untwist, 0, 0,
-                                                             fin_part);
-            if constexpr (G::NP > 1) __syncthreads();
-            uint32_t t2 = tau;
-            asm volatile("" : "+v"(t2));
-            fwd_poly<LOGN, NEGA, LAZY>(lds, v, t2, ct + 2 * G::N, valid, A);
-#pragma unroll
-            for (int e = 0; e < G::E; ++e)
-                v[e] = valid ? A.ar.mont(v[e], (W)E.key[G::N + gidx<LOGN, G::NP - 1>(t2, e)]) : W(0);
-            if constexpr (G::NP > 1) __syncthreads();
-            uint32_t t3 = tau;
-            asm volatile("" : "+v"(t3));
-            auto fin2 = [&](uint32_t gi, uint64_t x) -> uint64_t {
-                return final_fin(gi, valid ? subq(phase[gi], x, q) : 0);
-            };
-            inv_poly_from_regs<LOGN, NEGA, kPfSingle, false>(lds, v, t3, phase, valid, A, A.ninv, A.untwist, 0, 0,
-                                                             fin2);
-        } else {
-            auto fin1 = [&](uint32_t gi, uint64_t x) -> uint64_t {
-                return final_fin(gi, valid ? subq(red_q(ct[gi], q, mu), x, q) : 0);
-            };
-            inv_poly_from_regs<LOGN, NEGA, kPfSingle, false>(lds, v, tr, phase, valid, A, A.ninv, A.untwist, 0, 0,
-                                                             fin1);
-        }
+        const bool ntt = E.is_ntt;
+        auto fin = [&](uint32_t gi, uint64_t x) -> uint64_t {
+            return final_fin(gi, ntt ? x : (valid ? subq(red_q(ct[gi], q, mu), x, q) : 0));
+        };
+        inv_poly_from_regs<LOGN, NEGA, kPfSingle, false>(lds, v, tr, phase, valid, A, A.ninv, A.untwist, 0, 0, fin);
     }
     if (E.noise) {
         // max over the polynomial's lanes within the wave (a polynomial owns

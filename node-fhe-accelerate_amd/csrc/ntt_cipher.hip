@@ -25,6 +25,11 @@
 //                            inv(c1) -> row 1, inv(C) -> row 2
 // Products are Montgomery (x R^-1); the R is folded into the inverse's N^-1
 // (ninv_r), as in k_polymul.
+// streamed twiddles in the paired transforms (ntt_core.hpp FHE_STREAM_TW2):
+// 4.61 vs 4.67 ms per 16,384 ciphertext pairs (profiles/r3e/ab.txt)
+#ifndef FHE_STREAM_TW2
+#define FHE_STREAM_TW2 1
+#endif
 #include "fhe_internal.hpp"
 
 namespace FHE_NS {
@@ -69,11 +74,13 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 #ifndef FHE_CTMUL_AREG
 #define FHE_CTMUL_AREG 1
 #endif
-    // (u64: only where the VGPR slots fit without scratch spills -- at N =
-    // 4096/8192 they took 255 VGPRs plus scratch, and the N = 8192
-    // negacyclic build faulted on MI355X; the HBM-row slots with prefetch
-    // need 167-241 VGPRs and no scratch)
-    constexpr bool AREG = NL == 1 && FHE_CTMUL_AREG && sizeof(W) == 4;
+    // u64 as well (re-enabled r3; DESIGN.md section 9 "k_ct_mul fault"):
+    // the round-2 build of this layout at N = 8192 negacyclic (255 VGPRs, a
+    // 68 B private segment) was withdrawn after a fault report; its code
+    // object shows only constant-offset spill slots inside the segment and
+    // compile-time slot indices, and today's build of the same layout needs
+    // 205-221 VGPRs and no scratch (tests/test_abi.py keeps it that way).
+    constexpr bool AREG = NL == 1 && FHE_CTMUL_AREG;
     W areg[AREG ? G::E : 1];
     W breg[AREG ? G::E : 1];
     // HBM slots (NL < 3) hold W words in the first half of their u64 row
@@ -203,8 +210,8 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_wa
 k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *out, size_t batch,
           NttArgs<W> A) {
     using G = Geo<LOGN>;
-    static_assert(G::P == 1 && G::LOGE == 5, "one ciphertext pair per workgroup, 32 coefficients per thread");
-    constexpr int PF = 1;
+    static_assert(G::P == 1 && (G::LOGE == 5 || sizeof(W) == 8), "one ciphertext pair per workgroup");
+    constexpr int PF = sizeof(W) == 8 ? 0 : 1;  // u64: two 16-word spectra leave no VGPRs for lookahead
     __shared__ W lds[G::LW];
     const uint32_t tau = threadIdx.x;
     const size_t poly = blockIdx.x;
@@ -239,6 +246,8 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
         const W c1 = A.ar.red2q(A.ar.mont(s1[gi], b[e]) + A.ar.mont(x1, s2[gi]));
         b[e] = A.ar.mont(x1, b[e]);
         a[e] = c1;
+        // u64: 4 stash pairs in flight at a time (all 16 hoisted spill)
+        if (sizeof(W) == 8 && (e & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // every stash read precedes the final stores of rows 1 / 2
     uint32_t t3 = tau;
@@ -253,23 +262,28 @@ static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *
     const size_t blocks = (batch + G::P - 1) / G::P;
     bool lazy = false;
     if constexpr (sizeof(W) == 4) lazy = p.lazy;
-    if constexpr (sizeof(W) == 4 && (LOGN == 13 || LOGN == 14) && !FHE_CTMUL_E16) {
-        constexpr int K = gk(LOGN, 5);
-        if (lazy)
-            hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, true>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y, out,
-                               batch, A);
-        else
-            hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, false>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y,
-                               out, batch, A);
-        return hipGetLastError();
-    }
-    if (lazy) {
-        if constexpr (sizeof(W) == 4)
-            hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
-                               batch, A);
-    } else
-        hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, false>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
+    if constexpr ((sizeof(W) == 4 && (LOGN == 13 || LOGN == 14) && !FHE_CTMUL_E16) || (sizeof(W) == 8 && LOGN == 14)) {
+        // u64 at N = 16384: 16 coefficients per thread, the pairs in lockstep
+        // (no third slot in VGPRs: the single-transform kernel spilled there)
+        constexpr int K = sizeof(W) == 4 ? gk(LOGN, 5) : LOGN;
+        if constexpr (sizeof(W) == 4) {
+            if (lazy) {
+                hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, true>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y,
+                                   out, batch, A);
+                return hipGetLastError();
+            }
+        }
+        hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, false>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y, out,
                            batch, A);
+    } else {
+        if (lazy) {
+            if constexpr (sizeof(W) == 4)
+                hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y,
+                                   out, batch, A);
+        } else
+            hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, false>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
+                               batch, A);
+    }
     return hipGetLastError();
 }
 

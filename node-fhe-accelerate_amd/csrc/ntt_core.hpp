@@ -65,6 +65,22 @@ __host__ __device__ constexpr uint32_t pad_idx(uint32_t i) {
 template <int K>
 constexpr int lds_words() { return (int)pad_idx<K>((1u << gk_logn(K)) - 1) + 1; }
 
+// Split exchange (64-bit words at N = 16384, 32 coefficients per thread):
+// each pass exchange moves the
+// low 32-bit halves of the words through the LDS buffer, then the high halves
+// (store lo / sync / load lo / sync / store hi / sync / load hi), so the
+// buffer is 64 KiB instead of 128 KiB and two workgroups fit per CU -- one's
+// barriers and HBM waits overlap the other's butterflies.  Opt-in per
+// translation unit (FHE_SPLIT_X64 before the includes).
+#ifndef FHE_SPLIT_X64
+#define FHE_SPLIT_X64 0
+#endif
+template <int K, typename W>
+constexpr bool split_x() { return FHE_SPLIT_X64 && sizeof(W) == 8 && gk_logn(K) >= 14 && gk_loge(K) == 5; }
+// W-typed elements of one polynomial's exchange buffer
+template <int K, typename W>
+constexpr int lds_elems() { return split_x<K, W>() ? (lds_words<K>() + 1) / 2 : lds_words<K>(); }
+
 // ---------------------------------------------------------------- geometry
 template <int LOGN>
 struct Geo {
@@ -84,7 +100,7 @@ struct Geo {
     // allocation never costs a resident workgroup.
     template <typename W, int EXTRA_WORDS = 0>
     static constexpr int occ_waves() {
-        const int by_lds = (160 * 1024) / ((P * LW + EXTRA_WORDS) * (int)sizeof(W));
+        const int by_lds = (160 * 1024) / ((P * lds_elems<LOGN, W>() + EXTRA_WORDS) * (int)sizeof(W));
         const int by_thr = 2048 / THREADS;
         const int wg = by_lds < by_thr ? by_lds : by_thr;
         const int w = wg * THREADS / 64 / 4;
@@ -152,6 +168,36 @@ __device__ __forceinline__ void lds_load(const W *lds, W (&v)[Geo<LOGN>::E], uin
         for (int t = 0; t < (1 << R); ++t) v[t + (u << R)] = lds[base + pad_idx<LOGN>(uint32_t(t) << S)];
     }
 }
+// One pass exchange: registers in layout PA -> LDS -> registers in layout PB.
+// The caller's next exchange stores to the positions this one loaded from
+// (same thread, same layout), so no barrier is needed after the load.
+template <int LOGN, int PA, int PB, typename W>
+__device__ __forceinline__ void exchange(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau) {
+    constexpr int E = Geo<LOGN>::E;
+    if constexpr (split_x<LOGN, W>()) {
+        uint32_t *l32 = reinterpret_cast<uint32_t *>(lds);
+        uint32_t h[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) h[e] = (uint32_t)v[e];
+        lds_store<LOGN, PA>(l32, h, tau);
+#pragma unroll
+        for (int e = 0; e < E; ++e) h[e] = (uint32_t)(v[e] >> 32);
+        __syncthreads();
+        uint32_t lo[E];
+        lds_load<LOGN, PB>(l32, lo, tau);
+        __syncthreads();  // every lane's low halves read before the high halves overwrite them
+        lds_store<LOGN, PA>(l32, h, tau);
+        __syncthreads();
+        lds_load<LOGN, PB>(l32, h, tau);
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = (W)lo[e] | ((W)h[e] << 32);
+    } else {
+        lds_store<LOGN, PA>(lds, v, tau);
+        __syncthreads();
+        lds_load<LOGN, PB>(lds, v, tau);
+    }
+}
+
 // Global (natural-order) index of slot e in pass layout PASS (PASS > 0, or
 // the last pass): coalesced across tau.
 template <int LOGN, int PASS>
@@ -380,6 +426,147 @@ __device__ __forceinline__ void inv_stages(uint32_t tau, W (&v)[Geo<LOGN>::E], T
 template <int LOGN>
 constexpr bool staged_tw() { return Geo<LOGN>::LOGE >= 5; }
 
+// Streamed twiddles (64-bit words, 32 coefficients per thread): a radix-32
+// pass needs 31 Shoup pairs (124 VGPRs) per thread, which cannot sit beside a
+// 64-VGPR spectrum at two workgroups per CU.  The pass is instead walked as a
+// stream of its 31 butterfly groups (stage K, group tl: the 16 >> K
+// butterflies sharing twiddle slot 2^K - 1 + tl), each twiddle loaded SD
+// groups ahead of its single use, so only SD pairs are live.  The first SD
+// loads are issued before the pass's LDS exchange.
+#ifndef FHE_STREAM_TW
+#define FHE_STREAM_TW 1
+#endif
+#ifndef FHE_STREAM_DEPTH
+#define FHE_STREAM_DEPTH 4
+#endif
+template <int LOGN, typename W>
+constexpr bool stream_tw() { return FHE_STREAM_TW && sizeof(W) == 8 && Geo<LOGN>::LOGE == 5; }
+// Paired transforms (fwd_poly2 / inv_poly2) at 32 coefficients per thread
+// may stream their twiddles too (two 32-word spectra leave little room for
+// whole-stage twiddle sets).  Per translation unit: measured +1.3 % on the
+// ciphertext multiply (ntt_cipher.hip turns it on), -2 % on polymul.
+#ifndef FHE_STREAM_TW2
+#define FHE_STREAM_TW2 0
+#endif
+template <int LOGN, typename W>
+constexpr bool stream_tw2() { return FHE_STREAM_TW2 && Geo<LOGN>::LOGE == 5; }
+constexpr int kStreamDepth = FHE_STREAM_DEPTH;
+// 1: a pass's first SD twiddle loads are issued before its LDS exchange
+#ifndef FHE_STREAM_PRE
+#define FHE_STREAM_PRE 1
+#endif
+
+// Stream item i -> (stage k, slot group u, butterfly group tl): forward
+// items run stages 0..R-1, inverse items R-1..0; within a stage, slot group
+// then group ascending.
+struct SItem { int k, u, tl; };
+__host__ __device__ constexpr SItem stream_item(int R, int NU, bool inv, int i) {
+    for (int s = 0; s < R; ++s) {
+        const int k = inv ? R - 1 - s : s;
+        if (i < NU << k) return SItem{k, i >> k, i & ((1 << k) - 1)};
+        i -= NU << k;
+    }
+    return SItem{0, 0, 0};
+}
+
+// Twiddle (stage k, slot group u, group tl) for this lane (load_tw's
+// addressing for one slot).
+template <int LOGN, int PASS, typename W>
+__device__ __forceinline__ Tw<W> tw_one(uint32_t tau, const Tw<W> *__restrict__ tw, SItem it) {
+    using G = Geo<LOGN>;
+    constexpr int S = G::S(PASS);
+    if constexpr (PASS == 0) {  // S = 0: wave-uniform
+        typedef const __attribute__((address_space(4))) W cw_t;
+        const cw_t *cp = (const cw_t *)(const void *)tw;
+        const uint32_t idx = (1u << it.k) + uint32_t(it.tl);
+        return Tw<W>{cp[2 * idx], cp[2 * idx + 1]};
+    } else {
+        static_assert(G::P == 1, "streamed twiddles: one polynomial per workgroup");
+        constexpr uint32_t m = (1u << S) - 1;
+        const uint32_t cst = (1u << (S + it.k)) + ((uint32_t(it.u) << G::LOGT) & m) + (uint32_t(it.tl) << S);
+        return bload_tw<W>(brsrc(tw), (tau & m) * (uint32_t)sizeof(Tw<W>), cst * (uint32_t)sizeof(Tw<W>));
+    }
+}
+
+// Every item index is a template argument (compile-time twiddle slot and
+// register indices: a runtime index would put the arrays in scratch).
+template <int LOGN, int PASS, bool INV, bool SKIP0, int I, typename W>
+__device__ __forceinline__ void stream_load(uint32_t tau, const Tw<W> *__restrict__ tw,
+                                            Tw<W> (&b)[PassTw<LOGN, PASS>::COUNT]) {
+    using P = PassTw<LOGN, PASS>;
+    if constexpr (I < P::COUNT) {
+        constexpr SItem it = stream_item(P::R, P::NU, INV, I);
+        if constexpr (!(SKIP0 && it.k == 0))  // stage 0 of the transform: no twiddle (R-scaling / N^-1 folding)
+            b[I] = tw_one<LOGN, PASS>(tau, tw, it);
+    }
+}
+template <int LOGN, int PASS, bool INV, bool SKIP0, int I = 0, typename W>
+__device__ __forceinline__ void stream_begin(uint32_t tau, const Tw<W> *__restrict__ tw,
+                                             Tw<W> (&b)[PassTw<LOGN, PASS>::COUNT]) {
+    if constexpr (I < kStreamDepth) {
+        stream_load<LOGN, PASS, INV, SKIP0, I>(tau, tw, b);
+        stream_begin<LOGN, PASS, INV, SKIP0, I + 1>(tau, tw, b);
+    }
+}
+// Forward pass over the stream (stream_begin already issued).  RS: pass 0's
+// stage 0 multiplies by R (ct_rscale) instead of a twiddle.  D2: a second
+// spectrum *v2 takes the same butterflies (paired transforms, one twiddle
+// stream).
+template <int LOGN, int PASS, bool LAZY, bool RS, bool D2 = false, int I = 0, typename W>
+__device__ __forceinline__ void fwd_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&b)[PassTw<LOGN, PASS>::COUNT],
+                                                const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> rmod = Tw<W>{},
+                                                W (*v2)[Geo<LOGN>::E] = nullptr) {
+    using P = PassTw<LOGN, PASS>;
+    constexpr int R = P::R;
+    constexpr bool SK = RS && PASS == 0;
+    if constexpr (I < P::COUNT) {
+        stream_load<LOGN, PASS, false, SK, I + kStreamDepth>(tau, tw, b);
+        constexpr SItem it = stream_item(R, P::NU, false, I);
+        constexpr int k = it.k;
+#pragma unroll
+        for (int h = 0; h < (D2 ? 2 : 1); ++h) {
+            W (&x)[Geo<LOGN>::E] = h ? *v2 : v;
+#pragma unroll
+            for (int tt = 0; tt < (1 << R); ++tt) {
+                if ((tt & (1 << k)) || (tt & ((1 << k) - 1)) != it.tl) continue;
+                const int e = tt + (it.u << R), e2 = e + (1 << k);
+                if constexpr (SK && k == 0) ar.ct_rscale(x[e], x[e2], rmod);
+                else if constexpr (LAZY) ar.ct_lazy(x[e], x[e2], b[I]);
+                else ar.ct(x[e], x[e2], b[I]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        fwd_pass_stream<LOGN, PASS, LAZY, RS, D2, I + 1>(tau, v, b, tw, ar, rmod, v2);
+    }
+}
+// Inverse pass over the stream; FOLD: global stage 0 applies `scale`.
+template <int LOGN, int PASS, bool FOLD, bool D2 = false, int I = 0, typename W>
+__device__ __forceinline__ void inv_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&b)[PassTw<LOGN, PASS>::COUNT],
+                                                const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale,
+                                                W (*v2)[Geo<LOGN>::E] = nullptr) {
+    using P = PassTw<LOGN, PASS>;
+    constexpr int R = P::R;
+    constexpr bool SK = FOLD && PASS == 0;
+    if constexpr (I < P::COUNT) {
+        stream_load<LOGN, PASS, true, SK, I + kStreamDepth>(tau, tw, b);
+        constexpr SItem it = stream_item(R, P::NU, true, I);
+        constexpr int k = it.k;
+#pragma unroll
+        for (int h = 0; h < (D2 ? 2 : 1); ++h) {
+            W (&x)[Geo<LOGN>::E] = h ? *v2 : v;
+#pragma unroll
+            for (int tt = 0; tt < (1 << R); ++tt) {
+                if ((tt & (1 << k)) || (tt & ((1 << k) - 1)) != it.tl) continue;
+                const int e = tt + (it.u << R), e2 = e + (1 << k);
+                if constexpr (SK && k == 0) ar.gs_scaled(x[e], x[e2], scale);
+                else ar.gs(x[e], x[e2], b[I]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        inv_pass_stream<LOGN, PASS, FOLD, D2, I + 1>(tau, v, b, tw, ar, scale, v2);
+    }
+}
+
 // Passes PASS..NP-1 of the forward transform, exchanging through LDS.
 // hook() runs once, in the last pass after its twiddle loads are issued: the
 // place to start HBM loads for what follows the transform (VMEM counters
@@ -391,10 +578,17 @@ __device__ __forceinline__ void fwd_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
     using G = Geo<LOGN>;
     if constexpr (PASS < G::NP) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        if constexpr (stream_tw<LOGN, W>()) {
+            if constexpr (FHE_STREAM_PRE) stream_begin<LOGN, PASS, false, false>(tau, tw, t);  // in flight across the exchange
+            exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
+            if constexpr (!FHE_STREAM_PRE) stream_begin<LOGN, PASS, false, false>(tau, tw, t);
+            if constexpr (PASS == G::NP - 1) hook();
+            fwd_pass_stream<LOGN, PASS, LAZY, false>(tau, v, t, tw, ar);
+            fwd_rest<LOGN, PASS + 1, LAZY, PF>(lds, v, tau, tw, ar, hook);
+            return;
+        }
         load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);  // in flight across the exchange
-        lds_store<LOGN, PASS - 1>(lds, v, tau);
-        __syncthreads();
-        lds_load<LOGN, PASS>(lds, v, tau);
+        exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
         if constexpr (staged_tw<LOGN>()) {
             // stages 0..PF-1 issued before the exchange; stage K issues K+PF
             if constexpr (PASS == G::NP - 1) hook();
@@ -433,14 +627,19 @@ __device__ __forceinline__ void fwd_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     using G = Geo<LOGN>;
     if constexpr (PASS < G::NP) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        if constexpr (stream_tw2<LOGN, W>()) {
+            stream_begin<LOGN, PASS, false, false>(tau, tw, t);
+            exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
+            __syncthreads();
+            exchange<LOGN, PASS - 1, PASS>(lds, v2, tau);
+            fwd_pass_stream<LOGN, PASS, LAZY, false, true>(tau, v, t, tw, ar, Tw<W>{}, &v2);
+            fwd_rest2<LOGN, PASS + 1, LAZY, PF>(lds, v, v2, tau, tw, ar);
+            return;
+        }
         load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);
-        lds_store<LOGN, PASS - 1>(lds, v, tau);
+        exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
         __syncthreads();
-        lds_load<LOGN, PASS>(lds, v, tau);
-        __syncthreads();
-        lds_store<LOGN, PASS - 1>(lds, v2, tau);
-        __syncthreads();
-        lds_load<LOGN, PASS>(lds, v2, tau);
+        exchange<LOGN, PASS - 1, PASS>(lds, v2, tau);
         fwd_stages2<LOGN, PASS, 0, PF, LAZY>(tau, v, v2, t, tw, ar);
         fwd_rest2<LOGN, PASS + 1, LAZY, PF>(lds, v, v2, tau, tw, ar);
     }
@@ -452,13 +651,19 @@ __device__ __forceinline__ void inv_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
                                          const Arith<W> &ar, Tw<W> scale) {
     if constexpr (PASS >= 0) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        if constexpr (stream_tw<LOGN, W>()) {
+            if constexpr (FHE_STREAM_PRE) stream_begin<LOGN, PASS, true, FOLD && PASS == 0>(tau, tw, t);
+            exchange<LOGN, PASS + 1, PASS>(lds, v, tau);
+            if constexpr (!FHE_STREAM_PRE) stream_begin<LOGN, PASS, true, FOLD && PASS == 0>(tau, tw, t);
+            inv_pass_stream<LOGN, PASS, FOLD>(tau, v, t, tw, ar, scale);
+            inv_rest<LOGN, PASS - 1, FOLD, PF>(lds, v, tau, tw, ar, scale);
+            return;
+        }
         // inverse stages run k = R-1 .. 0: prefetch the top ones
         constexpr int R = PassTw<LOGN, PASS>::R;
         constexpr int KS = R - PF < 0 ? 0 : R - PF;
         load_tw<LOGN, PASS, W, KS, 8>(tau, tw, t);
-        lds_store<LOGN, PASS + 1>(lds, v, tau);
-        __syncthreads();
-        lds_load<LOGN, PASS>(lds, v, tau);
+        exchange<LOGN, PASS + 1, PASS>(lds, v, tau);
         if constexpr (staged_tw<LOGN>()) {
             // stages R-1..KS issued before the exchange; stage K issues K-PF
             inv_stages<LOGN, PASS, R - 1, R - KS, FOLD>(tau, v, t, tw, ar, scale);
@@ -649,8 +854,9 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
                                          bool valid, const NttArgs<W> &A, uint32_t sh = 0, uint32_t off = 0,
                                          H &&hook = NoHook{}, uint64_t (*pre)[Geo<LOGN>::E] = nullptr) {
     using G = Geo<LOGN>;
+    constexpr bool ST = stream_tw<LOGN, W>();
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
-    load_tw<LOGN, 0>(tau, A.twf, t0);
+    if constexpr (!ST) load_tw<LOGN, 0>(tau, A.twf, t0);
     // Shoup-based first steps (twist / R-scaling) accept any word
     const uint64_t lim = (NEGA || RS) ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     if (pre) {  // prefetched by the caller (load_raw)
@@ -671,7 +877,12 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
         for (int t = 0; t < G::E; ++t)
             v[t] = A.ar.shoup(v[t], A.twist[((tau + cbrv(t, G::LOGE) * G::T) << sh) | off]);
     }
-    fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
+    if constexpr (ST) {
+        stream_begin<LOGN, 0, false, RS>(tau, A.twf, t0);
+        fwd_pass_stream<LOGN, 0, LAZY, RS>(tau, v, t0, A.twf, A.ar, A.rmod);
+    } else {
+        fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
+    }
     fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar, hook);
 }
 
@@ -683,8 +894,9 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
                                           const NttArgs<W> &A) {
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
+    constexpr bool ST = stream_tw2<LOGN, W>();
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
-    load_tw<LOGN, 0>(tau, A.twf, t0);
+    if constexpr (!ST) load_tw<LOGN, 0>(tau, A.twf, t0);
     const uint64_t lim = NEGA ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     const uint32_t vo = tau * 8u;
     {
@@ -705,10 +917,17 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
             const Tw<W> tw = A.twist[tau + cbrv(t, G::LOGE) * G::T];
             v[t] = A.ar.shoup(v[t], tw);
             v2[t] = A.ar.shoup(v2[t], tw);
+            // u64: 4 twist pairs in flight at a time (16 hoisted = 64 VGPRs)
+            if (sizeof(W) == 8 && (t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
     }
-    fwd_pass<LOGN, 0, LAZY, W>(v, t0, A.ar);
-    fwd_pass<LOGN, 0, LAZY, W>(v2, t0, A.ar);
+    if constexpr (ST) {
+        stream_begin<LOGN, 0, false, false>(tau, A.twf, t0);
+        fwd_pass_stream<LOGN, 0, LAZY, false, true>(tau, v, t0, A.twf, A.ar, Tw<W>{}, &v2);
+    } else {
+        fwd_pass<LOGN, 0, LAZY, W>(v, t0, A.ar);
+        fwd_pass<LOGN, 0, LAZY, W>(v2, t0, A.ar);
+    }
     fwd_rest2<LOGN, 1, LAZY, PF>(lds, v, v2, tau, A.twf, A.ar);
 }
 
@@ -732,8 +951,13 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
     constexpr int LAST = G::NP - 1;
     {
         Tw<W> t[PassTw<LOGN, LAST>::COUNT];
-        load_tw<LOGN, LAST>(tau, A.twi, t);
-        inv_pass<LOGN, LAST, !NEGA>(v, t, A.ar, scale);
+        if constexpr (stream_tw<LOGN, W>()) {
+            stream_begin<LOGN, LAST, true, false>(tau, A.twi, t);
+            inv_pass_stream<LOGN, LAST, !NEGA>(tau, v, t, A.twi, A.ar, scale);
+        } else {
+            load_tw<LOGN, LAST>(tau, A.twi, t);
+            inv_pass<LOGN, LAST, !NEGA>(v, t, A.ar, scale);
+        }
     }
     inv_rest<LOGN, LAST - 1, !NEGA, PF>(lds, v, tau, A.twi, A.ar, scale);
 #pragma unroll
@@ -771,16 +995,21 @@ __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
                                           const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale) {
     if constexpr (PASS >= 0) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        if constexpr (stream_tw2<LOGN, W>()) {
+            stream_begin<LOGN, PASS, true, FOLD && PASS == 0>(tau, tw, t);
+            exchange<LOGN, PASS + 1, PASS>(lds, v, tau);
+            __syncthreads();
+            exchange<LOGN, PASS + 1, PASS>(lds, v2, tau);
+            inv_pass_stream<LOGN, PASS, FOLD, true>(tau, v, t, tw, ar, scale, &v2);
+            inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);
+            return;
+        }
         constexpr int R = PassTw<LOGN, PASS>::R;
         constexpr int KS = R - PF < 0 ? 0 : R - PF;
         load_tw<LOGN, PASS, W, KS, 8>(tau, tw, t);
-        lds_store<LOGN, PASS + 1>(lds, v, tau);
+        exchange<LOGN, PASS + 1, PASS>(lds, v, tau);
         __syncthreads();
-        lds_load<LOGN, PASS>(lds, v, tau);
-        __syncthreads();
-        lds_store<LOGN, PASS + 1>(lds, v2, tau);
-        __syncthreads();
-        lds_load<LOGN, PASS>(lds, v2, tau);
+        exchange<LOGN, PASS + 1, PASS>(lds, v2, tau);
         inv_stages2<LOGN, PASS, R - 1, R - KS, FOLD>(tau, v, v2, t, tw, ar, scale);
         inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);
     }
@@ -795,10 +1024,15 @@ __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     constexpr int LAST = G::NP - 1;
     {
         Tw<W> t[PassTw<LOGN, LAST>::COUNT];
-        constexpr int R = PassTw<LOGN, LAST>::R;
-        constexpr int KS = R - PF < 0 ? 0 : R - PF;
-        load_tw<LOGN, LAST, W, KS, 8>(tau, A.twi, t);
-        inv_stages2<LOGN, LAST, R - 1, R - KS, !NEGA>(tau, v, v2, t, A.twi, A.ar, scale);
+        if constexpr (stream_tw2<LOGN, W>()) {
+            stream_begin<LOGN, LAST, true, false>(tau, A.twi, t);
+            inv_pass_stream<LOGN, LAST, !NEGA, true>(tau, v, t, A.twi, A.ar, scale, &v2);
+        } else {
+            constexpr int R = PassTw<LOGN, LAST>::R;
+            constexpr int KS = R - PF < 0 ? 0 : R - PF;
+            load_tw<LOGN, LAST, W, KS, 8>(tau, A.twi, t);
+            inv_stages2<LOGN, LAST, R - 1, R - KS, !NEGA>(tau, v, v2, t, A.twi, A.ar, scale);
+        }
     }
     inv_rest2<LOGN, LAST - 1, !NEGA, PF>(lds, v, v2, tau, A.twi, A.ar, scale);
     const auto r1 = brsrc(dst), r2 = brsrc(dst2);
@@ -812,6 +1046,7 @@ __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         }
         bstore(r1, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin1(gi, (uint64_t)A.ar.red1q(x)));
         bstore(r2, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin2(gi, (uint64_t)A.ar.red1q(x2)));
+        if (NEGA && sizeof(W) == 8 && (t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
 }
 

@@ -9,6 +9,13 @@
 #ifndef FHE_U64_NOVCC
 #define FHE_U64_NOVCC 1
 #endif
+#ifndef FHE_SPLIT_X64
+#define FHE_SPLIT_X64 1
+#endif
+// streamed twiddles one group ahead: depth 2+ spills 8-12 B at 128 VGPRs
+#ifndef FHE_STREAM_DEPTH
+#define FHE_STREAM_DEPTH 1
+#endif
 #include "fhe_internal.hpp"
 
 namespace FHE_NS {
@@ -17,11 +24,11 @@ template <int LOGN, typename W, bool NEGA, bool LAZY, int EPI>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::LW];
+    __shared__ W lds_all[G::P * lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::LW;
+    W *lds = lds_all + pl * lds_elems<LOGN, W>();
     if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped
     W v[G::E];
     // EPI 1: transform times R (Montgomery form), folded into stage 0
@@ -50,11 +57,11 @@ __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_wa
 k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
               size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::LW];
+    __shared__ W lds_all[G::P * lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::LW;
+    W *lds = lds_all + pl * lds_elems<LOGN, W>();
     if (G::P == 1 && !valid) return;
     W v[G::E];
     // fwd(a) * R (stage 0 scaled), so mont(fwd(a)R, w) = fwd(a) w; the raw
@@ -63,7 +70,7 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
     const uint64_t *wp = wv + poly * G::N;
     uint64_t *dst = out + poly * G::N;
 #if FHE_FWDMUL_PREFETCH
-    if constexpr (G::P == 1) {
+    if constexpr (G::P == 1 && G::E <= 16) {  // 32 raw u64 words would not fit beside the spectrum
         // w is loaded during the last pass (its HBM latency overlaps it)
         uint64_t rw[G::E];
         const uint32_t vo = LastIO<LOGN>::vo(tau);
@@ -109,9 +116,19 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
     }
 }
 
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+// 64-bit words at N = 16384: 32 coefficients per thread (512 threads,
+// radix-32 passes: 2 exchanges instead of 3) and the split exchange, so two
+// workgroups share a CU at <= 128 VGPRs each.
+#ifndef FHE_FWD64_E32
+#define FHE_FWD64_E32 1
+#endif
+template <int LOGN, typename W>
+constexpr int fwd_key() { return (FHE_FWD64_E32 && sizeof(W) == 8 && LOGN == 14) ? gk(LOGN, 5) : LOGN; }
+
+template <int LOGN0, typename W, bool NEGA, bool LAZY>
 static hipError_t fwd_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *in, uint64_t *out, size_t batch,
                           int epi, const uint64_t *wv) {
+    constexpr int LOGN = fwd_key<LOGN0, W>();
     using G = Geo<LOGN>;
     const size_t blocks = (batch + G::P - 1) / G::P;
     if (wv)

@@ -4,6 +4,9 @@
 // inv(fwd(a) (.) fwd(b)) in ONE kernel: both spectra stay in VGPRs, the
 // pointwise product is a Montgomery multiply whose R^-1 is folded into the
 // inverse's N^-1 scaling).
+#ifndef FHE_SPLIT_X64
+#define FHE_SPLIT_X64 1
+#endif
 #include "fhe_internal.hpp"
 
 namespace FHE_NS {
@@ -12,11 +15,11 @@ template <int LOGN, typename W, bool NEGA>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
-    __shared__ W lds_all[G::P * G::LW];
+    __shared__ W lds_all[G::P * lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::LW;
+    W *lds = lds_all + pl * lds_elems<LOGN, W>();
     if (G::P == 1 && !valid) return;
     W v[G::E];
     const uint64_t *src = in + poly * G::N;
@@ -52,6 +55,7 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 template <int LOGN, typename W>
 constexpr int polymul_stash() {
     using G = Geo<LOGN>;
+    if (G::LOGE == 5 && sizeof(W) == 8) return 2;  // 64-bit words: two 64-word spectra do not fit
     if (G::L < 5 || G::LOGE == 5) return 0;  // 32 coefficients per thread: fwd(a) stays in VGPRs
     if (FHE_POLY_REG_STASH_14 && G::L == 14 && sizeof(W) == 4) return 0;
     if (FHE_POLY_HBM_STASH && G::L == 14) return 2;
@@ -61,7 +65,8 @@ template <int LOGN, typename W>
 constexpr int polymul_occ() {
     // with the stash in HBM the LDS footprint admits a second workgroup
     if (polymul_stash<LOGN, W>() == 0 && Geo<LOGN>::L >= 12) return Geo<LOGN>::template occ_waves<W>();
-    return polymul_stash<LOGN, W>() == 2 && FHE_POLY_HBM_STASH ? Geo<LOGN>::template occ_waves<W>() : 1;
+    return polymul_stash<LOGN, W>() == 2 && (FHE_POLY_HBM_STASH || Geo<LOGN>::LOGE == 5)
+               ? Geo<LOGN>::template occ_waves<W>() : 1;
 }
 // Polymul geometry: at q < 2^30 and N >= 4096, 32 coefficients per thread
 // (radix-32 passes: 2 LDS exchanges per transform instead of 3, N/32 threads,
@@ -74,12 +79,48 @@ constexpr int polymul_occ() {
 #ifndef FHE_PF_POLY32
 #define FHE_PF_POLY32 1
 #endif
+// 64-bit words at N = 16384 (FHE_POLY64): 1 = the dual kernel at 16
+// coefficients per thread (one workgroup per CU, 128 VGPRs, no stash);
+// 2 = 32 per thread with streamed twiddles, the split exchange and fwd(a)
+// stashed in c's row (two workgroups per CU, 1.67x the algorithmic bytes).
+#ifndef FHE_POLY64
+#define FHE_POLY64 1
+#endif
+// Inverse transform key: FHE_INV64_E32=1 runs 64-bit words at N = 16384 at
+// 32 coefficients per thread with streamed twiddles and the split exchange
+// (as the forward).  Measured slower than 16 per thread (7.91 vs 7.62 ms per
+// 65,536 inverses, profiles/r3e/ab.txt), so off.
+#ifndef FHE_INV64_E32
+#define FHE_INV64_E32 0
+#endif
+template <int LOGN, typename W>
+constexpr int inv_key() { return (FHE_INV64_E32 && sizeof(W) == 8 && LOGN == 14) ? gk(LOGN, 5) : LOGN; }
 template <int LOGN, typename W>
 constexpr int polymul_key() {
+    if (sizeof(W) == 8) return (FHE_POLY64 == 2 && LOGN == 14) ? gk(LOGN, 5) : LOGN;
     return (!FHE_POLY_E16 && sizeof(W) == 4 && LOGN >= 13 && LOGN <= 14) ? gk(LOGN, 5) : LOGN;
 }
 template <int LOGN>
 constexpr int polymul_pf() { return Geo<LOGN>::LOGE == 5 ? FHE_PF_POLY32 : kPfPolymul; }
+// 64-bit words at N = 16384: the dual kernel at 16 coefficients per thread
+// (two 16-word u64 spectra = 64 VGPRs; no stash of fwd(a) in LDS or HBM).
+#ifndef FHE_POLY_DUAL
+#define FHE_POLY_DUAL 1
+#endif
+#ifndef FHE_POLY_DUAL64
+#define FHE_POLY_DUAL64 1
+#endif
+#ifndef FHE_PF_DUAL64
+#define FHE_PF_DUAL64 0
+#endif
+template <int LOGN, typename W>
+constexpr bool polymul_dual() {
+    using G = Geo<LOGN>;
+    if constexpr (sizeof(W) == 4) return G::LOGE == 5 && FHE_POLY_DUAL;
+    else return FHE_POLY_DUAL64 && G::P == 1 && G::L == 14 && G::LOGE == 4 && FHE_POLY64 == 1;
+}
+template <int LOGN, typename W>
+constexpr int polymul2_pf() { return sizeof(W) == 8 ? FHE_PF_DUAL64 : polymul_pf<LOGN>(); }
 
 template <int LOGN, typename W, bool NEGA, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
@@ -87,12 +128,12 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
           NttArgs<W> A) {
     using G = Geo<LOGN>;
     constexpr int STASH = polymul_stash<LOGN, W>();
-    __shared__ W lds_all[G::P * G::LW + (STASH == 1 ? G::P * G::N : 0)];
+    __shared__ W lds_all[G::P * lds_elems<LOGN, W>() + (STASH == 1 ? G::P * G::N : 0)];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
     const size_t poly = (size_t)blockIdx.x * G::P + pl;
     const bool valid = poly < batch;
-    W *lds = lds_all + pl * G::LW;
-    W *st = lds_all + G::P * G::LW + pl * G::N;
+    W *lds = lds_all + pl * lds_elems<LOGN, W>();
+    W *st = lds_all + G::P * lds_elems<LOGN, W>() + pl * G::N;
     uint64_t *crow = c + poly * G::N;
     if (G::P == 1 && !valid) return;
     W v[G::E];
@@ -149,42 +190,41 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
 // then the pointwise Montgomery product and the inverse.  Two workgroups per
 // CU (one 64 KiB exchange buffer each), so one's HBM traffic overlaps the
 // other's transforms.
-#ifndef FHE_POLY_DUAL
-#define FHE_POLY_DUAL 1
-#endif
 template <int LOGN, typename W, bool NEGA, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
            NttArgs<W> A) {
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "one polynomial pair per workgroup");
-    __shared__ W lds[G::LW];
+    __shared__ W lds[lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x;
     const size_t poly = blockIdx.x;
     if (poly >= batch) return;
     W v[G::E], vb[G::E];
-    fwd_poly2<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, vb, tau, a + poly * G::N, b + poly * G::N, A);
+    fwd_poly2<LOGN, NEGA, LAZY, polymul2_pf<LOGN, W>()>(lds, v, vb, tau, a + poly * G::N, b + poly * G::N, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) v[e] = A.ar.mont(fwd_to_canon<LAZY>(v[e], A), vb[e]);  // canonical x raw (< R)
     __syncthreads();  // the exchange buffer still holds b's last layout reads
-    inv_poly_from_regs<LOGN, NEGA, polymul_pf<LOGN>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, NEGA, polymul2_pf<LOGN, W>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r, A.untwist_r);
 }
 
 template <int LOGN, typename W, bool NEGA>
 static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, const uint64_t *a, const uint64_t *b,
                           uint64_t *c, size_t batch) {
-    using G = Geo<LOGN>;
-    const size_t blocks = (batch + G::P - 1) / G::P;
     bool lazy = false;
     if constexpr (sizeof(W) == 4) lazy = p.lazy;
     constexpr int PK = polymul_key<LOGN, W>();
     using GP = Geo<PK>;
     const size_t pblocks = (batch + GP::P - 1) / GP::P;
-    if constexpr (GP::LOGE == 5 && FHE_POLY_DUAL && sizeof(W) == 4) {
+    if constexpr (polymul_dual<PK, W>()) {
         if (b) {
-            if (lazy)
-                hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
-            else
+            if constexpr (sizeof(W) == 4) {
+                if (lazy) {
+                    hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b,
+                                       c, batch, A);
+                    return hipGetLastError();
+                }
+            }
                 hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
             return hipGetLastError();
         }
@@ -199,7 +239,10 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
         }
     }
     {
-        hipLaunchKernelGGL((k_ntt_inv<LOGN, W, NEGA>), dim3(blocks), dim3(G::THREADS), 0, s, a, c, batch, A);
+        constexpr int IK = inv_key<LOGN, W>();
+        using GI = Geo<IK>;
+        const size_t iblocks = (batch + GI::P - 1) / GI::P;
+        hipLaunchKernelGGL((k_ntt_inv<IK, W, NEGA>), dim3(iblocks), dim3(GI::THREADS), 0, s, a, c, batch, A);
     }
     return hipGetLastError();
 }

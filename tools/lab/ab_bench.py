@@ -21,6 +21,7 @@ ap.add_argument("--qs", default="132120577,4611686018326724609")
 ap.add_argument("--n", type=int, default=16384)
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--mode", default="compat")
 args = ap.parse_args()
 n, B = args.n, args.batch
 for q in [int(x) for x in args.qs.split(",")]:
@@ -28,7 +29,7 @@ for q in [int(x) for x in args.qs.split(",")]:
     a = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
     b = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
     out = torch.empty_like(a)
-    ring = fhe_gpu.PolynomialRing(n, q)
+    ring = fhe_gpu.PolynomialRing(n, q, mode=args.mode)
     eps = {}
     for bl, lv in ((23, 1), (15, 2)):
         ggsw = torch.randint(0, q, (2 * lv, 2, n), device="cuda", dtype=torch.int64, generator=g)
@@ -60,6 +61,7 @@ for q in [int(x) for x in args.qs.split(",")]:
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.steps
-        print(f"AB {args.tag} {op} {q} {ms:.4f} {chk}", flush=True)
+        qtag = q if args.mode == "compat" else f"{q}/{args.mode}"
+        print(f"AB {args.tag} {op} {qtag} {ms:.4f} {chk}", flush=True)
     del a, b, out
     torch.cuda.empty_cache()
