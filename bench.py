@@ -495,6 +495,8 @@ def pmc_traffic(kernel, n, batch, q, mode="compat"):
         # 32 coefficients per thread, paired forward transforms (geometry key
         # logN | 5 << 8; ntt_inv.hip k_polymul2)
         sym = f"k_polymul2<{logn | (5 << 8)}, {word},"
+    elif kernel == "polymul" and q >= (1 << 30) and logn == 14:
+        sym = f"k_polymul2<{logn}, {word},"  # 64-bit words: paired, 16 per thread
     best = None
     for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
         try:

@@ -92,7 +92,7 @@ constexpr int eng_occ() {
     return Geo<LOGN>::template occ_waves<W, eng_stash<LOGN, W>() == 1 ? Geo<LOGN>::P * Geo<LOGN>::N : 0>();
 }
 
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (eng_occ<LOGN, W>()))
 k_encrypt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -109,7 +109,7 @@ k_encrypt(EngArgs E, NttArgs<W> A) {
     const uint64_t q = A.q64, mu = A.mu64;
     W v[G::E];
     W va[STASH == 0 ? G::E : 1];
-    fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, E.u + row, valid, A);
+    fwd_poly<LOGN, LAZY>(lds, v, tau, E.u + row, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
@@ -128,7 +128,7 @@ k_encrypt(EngArgs E, NttArgs<W> A) {
             if (!valid) return 0;
             return addq(addq(x, red_q(E.e1[row + gi], q, mu), q), encode1(E.vals[row + gi], E.D), q);
         };
-        inv_poly_from_regs<LOGN, NEGA>(lds, v, tr, c0, valid, A, A.ninv, A.untwist, 0, 0, fin0);
+        inv_poly_from_regs<LOGN>(lds, v, tr, c0, valid, A, A.ninv, 0, fin0);
     }
     if constexpr (G::NP > 1) __syncthreads();
     uint32_t tb = tau;
@@ -144,7 +144,7 @@ k_encrypt(EngArgs E, NttArgs<W> A) {
     auto fin1 = [&](uint32_t gi, uint64_t x) -> uint64_t {
         return valid ? addq(x, red_q(E.e2[row + gi], q, mu), q) : 0;
     };
-    inv_poly_from_regs<LOGN, NEGA>(lds, v, tb, c1, valid, A, A.ninv, A.untwist, 0, 0, fin1);
+    inv_poly_from_regs<LOGN>(lds, v, tb, c1, valid, A, A.ninv, 0, fin1);
 }
 
 // decrypt and add_plain: at most 4 waves per SIMD (128 VGPRs): the
@@ -164,7 +164,7 @@ constexpr int dec_occ() {
     return (sizeof(W) == 8 && Geo<LOGN>::L >= 8 && Geo<LOGN>::L <= 11) ? 2 : eng_occ4<LOGN, W>();
 }
 
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (dec_occ<LOGN, W>()))
 k_decrypt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -213,7 +213,7 @@ k_decrypt(EngArgs E, NttArgs<W> A) {
         for (int c = 1; c < E.comps; ++c) {
             uint32_t tc = tau;
             asm volatile("" : "+v"(tc));
-            fwd_poly<LOGN, NEGA, LAZY>(lds, v, tc, ct + (size_t)c * G::N, valid, A);
+            fwd_poly<LOGN, LAZY>(lds, v, tc, ct + (size_t)c * G::N, valid, A);
             const bool last = c + 1 == E.comps;
 #pragma unroll
             for (int e = 0; e < G::E; ++e) {
@@ -233,7 +233,7 @@ k_decrypt(EngArgs E, NttArgs<W> A) {
         auto fin = [&](uint32_t gi, uint64_t x) -> uint64_t {
             return final_fin(gi, ntt ? x : (valid ? subq(red_q(ct[gi], q, mu), x, q) : 0));
         };
-        inv_poly_from_regs<LOGN, NEGA, kPfSingle, false>(lds, v, tr, phase, valid, A, A.ninv, A.untwist, 0, 0, fin);
+        inv_poly_from_regs<LOGN, kPfSingle, false>(lds, v, tr, phase, valid, A, A.ninv, 0, fin);
     }
     if (E.noise) {
         // max over the polynomial's lanes within the wave (a polynomial owns
@@ -252,7 +252,7 @@ k_decrypt(EngArgs E, NttArgs<W> A) {
 }
 
 // add_plain on NTT-domain ciphertexts: c0 + fwd(encode(values)), c1 copied.
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (eng_occ4<LOGN, W>()))
 k_add_plain_ntt(EngArgs E, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -269,7 +269,7 @@ k_add_plain_ntt(EngArgs E, NttArgs<W> A) {
     for (int t = 0; t < G::E; ++t)
         raw[t] = valid ? encode1(E.vals[row + tau + cbrv(t, G::LOGE) * G::T], E.D) : 0;
     W v[G::E];
-    fwd_poly<LOGN, NEGA, LAZY>(lds, v, tau, nullptr, valid, A, 0, 0, NoHook{}, &raw);
+    fwd_poly<LOGN, LAZY>(lds, v, tau, nullptr, valid, A, 0, NoHook{}, &raw);
     if (!valid) return;
     const uint64_t *c = E.ct + 2 * row;
     uint64_t *o = E.out + 2 * row;
@@ -283,29 +283,29 @@ k_add_plain_ntt(EngArgs E, NttArgs<W> A) {
 
 // Template dispatch over (logN, word, mode, lazy) for one kernel family;
 // each ntt_engine_*.hip instantiates one family (parallel compile units).
-template <int OP, int LOGN, typename W, bool NEGA, bool LAZY>
+template <int OP, int LOGN, typename W, bool LAZY>
 static hipError_t eng_one(const NttArgs<W> &A, hipStream_t s, const EngArgs &E) {
     using G = Geo<LOGN>;
     const size_t blocks = (E.batch + G::P - 1) / G::P;
     if constexpr (OP == 0)
-        hipLaunchKernelGGL((k_encrypt<LOGN, W, NEGA, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, E, A);
+        hipLaunchKernelGGL((k_encrypt<LOGN, W, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, E, A);
     else if constexpr (OP == 1)
-        hipLaunchKernelGGL((k_decrypt<LOGN, W, NEGA, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, E, A);
+        hipLaunchKernelGGL((k_decrypt<LOGN, W, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, E, A);
     else
-        hipLaunchKernelGGL((k_add_plain_ntt<LOGN, W, NEGA, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, E, A);
+        hipLaunchKernelGGL((k_add_plain_ntt<LOGN, W, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, E, A);
     return hipGetLastError();
 }
-template <int OP, int LOGN, typename W, bool NEGA>
+template <int OP, int LOGN, typename W>
 static hipError_t eng_lazy(const Plan &p, const NttArgs<W> &A, const EngArgs &E) {
     if constexpr (sizeof(W) == 4)
-        if (p.lazy) return eng_one<OP, LOGN, W, NEGA, true>(A, p.stream, E);
-    return eng_one<OP, LOGN, W, NEGA, false>(A, p.stream, E);
+        if (p.lazy) return eng_one<OP, LOGN, W, true>(A, p.stream, E);
+    return eng_one<OP, LOGN, W, false>(A, p.stream, E);
 }
-template <int OP, typename W, bool NEGA>
+template <int OP, typename W>
 static hipError_t eng_dispatch(const Plan &p, const NttArgs<W> &A, const EngArgs &E) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return eng_lazy<OP, L, W, NEGA>(p, A, E);
+    case L: return eng_lazy<OP, L, W>(p, A, E);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -316,8 +316,8 @@ template <int OP>
 static hipError_t eng_any(const Plan &p, const EngArgs &E) {
     if (E.batch == 0) return hipSuccess;
     if (p.word == 32)
-        return p.nega ? eng_dispatch<OP, uint32_t, true>(p, p.a32, E) : eng_dispatch<OP, uint32_t, false>(p, p.a32, E);
-    return p.nega ? eng_dispatch<OP, uint64_t, true>(p, p.a64, E) : eng_dispatch<OP, uint64_t, false>(p, p.a64, E);
+        return eng_dispatch<OP, uint32_t>(p, p.a32, E);
+    return eng_dispatch<OP, uint64_t>(p, p.a64, E);
 }
 
 static inline Decoder make_decoder(uint64_t q, uint64_t t) {

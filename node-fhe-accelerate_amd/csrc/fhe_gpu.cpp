@@ -84,7 +84,7 @@ FHE_NS::Tw<W> make_tw(u64 w, u64 q) {
 
 // ---------------------------------------------------------------- context
 struct Tables {
-    void *twf = nullptr, *twi = nullptr, *twist = nullptr, *untwist = nullptr, *untwist_r = nullptr;
+    void *twf = nullptr, *twi = nullptr;
 };
 
 }  // namespace
@@ -174,12 +174,18 @@ int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
     const u32 n = c->n, L = c->logn;
     const u64 q = c->q;
     constexpr int BITS = sizeof(W) * 8;
-    std::vector<FHE_NS::Tw<W>> twf(n), twi(n), twist(n), untw(n), untw_r(n);
-    // stage-major: entry 2^s + j holds the twiddle of butterfly j in stage s
+    std::vector<FHE_NS::Tw<W>> twf(n), twi(n);
+    // stage-major: entry 2^s + j holds the twiddle of butterfly j in stage s.
+    // compat: psi^(j*N/2^(s+1)) (ntt_processor.cpp:283-286).  negacyclic:
+    // psi^((2j+1)*N/2^(s+1)) -- the cyclic transform of the psi^i-twisted
+    // input, X_k = sum_i a_i psi^(i(2k+1)), with the twist merged into the
+    // stages (stage s of size 2m = 2^(s+1) is a negacyclic transform with
+    // root psi^(N/2m), so its butterfly j takes that root to the 2j+1).  The
+    // inverse table holds the inverse of every entry, so the same kernels
+    // (and the N^-1 fold) serve both modes, with no twist or untwist pass.
     for (u32 s = 0; s < L; ++s) {
         for (u32 j = 0; j < (1u << s); ++j) {
-            // compat: psi^(j*N/2^(s+1)); negacyclic: (psi^2)^(j*N/2^(s+1))
-            const u64 ex = c->mode == FHE_MODE_COMPAT ? (u64)j * (n >> (s + 1)) : (u64)j * (n >> s);
+            const u64 ex = c->mode == FHE_MODE_COMPAT ? (u64)j * (n >> (s + 1)) : (u64)(2 * j + 1) * (n >> (s + 1));
             twf[(1u << s) + j] = make_tw<W>(c->fwd_tw[ex], q);
             twi[(1u << s) + j] = make_tw<W>(c->inv_tw[ex], q);
         }
@@ -190,24 +196,15 @@ int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
         for (auto &t : twf) t.w = (W)(0u - t.w);  // Arith::ct's negated-twiddle butterfly
     const u64 R = (u64)((((u128)1) << BITS) % q);
     const u64 ninv_r = mulmod(c->inv_n, R, q);
-    for (u32 i = 0; i < n; ++i) {
-        twist[i] = make_tw<W>(c->fwd_tw[i], q);
-        const u64 u = mulmod(c->inv_tw[i], c->inv_n, q);
-        untw[i] = make_tw<W>(u, q);
-        untw_r[i] = make_tw<W>(mulmod(u, R, q), q);
-    }
     const size_t bytes = sizeof(FHE_NS::Tw<W>) * n;
-    void **dst[5] = {&c->tab.twf, &c->tab.twi, &c->tab.twist, &c->tab.untwist, &c->tab.untwist_r};
-    const void *srcs[5] = {twf.data(), twi.data(), twist.data(), untw.data(), untw_r.data()};
-    for (int i = 0; i < 5; ++i) {
+    void **dst[2] = {&c->tab.twf, &c->tab.twi};
+    const void *srcs[2] = {twf.data(), twi.data()};
+    for (int i = 0; i < 2; ++i) {
         HIP_TRY(hipMalloc(dst[i], bytes), "hipMalloc(twiddles)");
         HIP_TRY(hipMemcpy(*dst[i], srcs[i], bytes, hipMemcpyHostToDevice), "hipMemcpy(twiddles)");
     }
     A.twf = (const FHE_NS::Tw<W> *)c->tab.twf;
     A.twi = (const FHE_NS::Tw<W> *)c->tab.twi;
-    A.twist = (const FHE_NS::Tw<W> *)c->tab.twist;
-    A.untwist = (const FHE_NS::Tw<W> *)c->tab.untwist;
-    A.untwist_r = (const FHE_NS::Tw<W> *)c->tab.untwist_r;
     A.ar.q = (W)q;
     A.ar.q2 = (W)(2 * q);
     A.ar.qinv = neg_inv_pow2<W>((W)q);
@@ -239,7 +236,7 @@ void free_pipe(fhe_ctx *c) {
 }
 
 void free_tables(fhe_ctx *c) {
-    void *p[5] = {c->tab.twf, c->tab.twi, c->tab.twist, c->tab.untwist, c->tab.untwist_r};
+    void *p[2] = {c->tab.twf, c->tab.twi};
     for (void *x : p)
         if (x) (void)hipFree(x);
     c->tab = Tables{};
@@ -762,7 +759,6 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     c->stream = c->own_stream;
     c->plan.logn = logn;
     c->plan.word = c->word;
-    c->plan.nega = mode;
     c->plan.lazy = c->word == 32 && (u128)(4 + 2 * logn) * q <= ((u128)1 << 32);
     c->plan.stream = c->stream;
     c->plan.big_sync = &c->big_sync;

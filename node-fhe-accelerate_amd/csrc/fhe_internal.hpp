@@ -25,7 +25,6 @@ struct BigSync {
 struct Plan {
     uint32_t logn;
     int word;   // 32 or 64
-    int nega;   // 0 = compat, 1 = negacyclic
     int lazy;   // 32-bit path with (4 + 2L) q <= 2^32: forward stages skip reductions
     hipStream_t stream;
     // N > 2^kMaxFusedLogN (ntt_big.hip): two chunk-sized scratch buffers
@@ -53,6 +52,11 @@ hipError_t launch_big(const Plan &p, int op, const uint64_t *a, const uint64_t *
 // TFHE external product, GGSW already in NTT-Montgomery form.
 hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const uint64_t *glwe,
                           const uint64_t *ggsw, uint64_t *out, size_t batch);
+// Several decomposition levels at N = 16384, 64-bit words, k1 == 2,
+// base_log <= 31 (ntt_ext2.hip): accumulators in VGPRs, one HBM pass.
+bool extprod_acc_supported(const Plan &p, int k1, int level, int base_log);
+hipError_t launch_extprod_acc(const Plan &p, int level, int base_log, const uint64_t *glwe, const uint64_t *ggsw,
+                              uint64_t *out, size_t batch);
 
 // Relinearisation (EncryptionEngine::relinearize): ct3 [batch][3][n],
 // rlk [level][2][n] (a_l, b_l) in NTT-Montgomery form -> out [batch][2][n].

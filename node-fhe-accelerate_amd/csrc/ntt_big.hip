@@ -42,7 +42,7 @@ __device__ __forceinline__ void big_map(size_t &poly, uint32_t &b) {
 static size_t big_blocks(size_t batch, int M) { return ((batch + 7) / 8) * 8 << M; }
 
 // ---------------------------------------------------------------- rows
-template <int M, typename W, bool NEGA, bool LAZY>
+template <int M, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<kBigS>::THREADS, Geo<kBigS>::template occ_waves<W>())
 k_big_fwd_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<kBigS>;
@@ -55,14 +55,14 @@ k_big_fwd_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size
     if (!valid) return;  // whole workgroup (P == 1)
     const uint32_t tau = threadIdx.x, o = cbrv(b, M);
     W v[G::E];
-    fwd_poly<kBigS, NEGA, LAZY>(lds, v, tau, in + (poly << (kBigS + M)) + o, valid, A, M, o);
+    fwd_poly<kBigS, LAZY>(lds, v, tau, in + (poly << (kBigS + M)) + o, valid, A, M);
     const auto r = brsrc(out + (poly << (kBigS + M)) + ((size_t)b << kBigS));
     const uint32_t vo = LastIO<kBigS>::vo(tau);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) bstore(r, vo, LastIO<kBigS>::so(e), (uint64_t)fwd_to_canon<LAZY>(v[e], A));
 }
 
-template <int M, typename W, bool NEGA, bool MONT>
+template <int M, typename W, bool MONT>
 __global__ void __launch_bounds__(Geo<kBigS>::THREADS, Geo<kBigS>::template occ_waves<W>())
 k_big_inv_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<kBigS>;
@@ -78,8 +78,8 @@ k_big_inv_rows(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size
     W v[G::E];
     load_coeffs_r<G::E>(v, (uint64_t)A.ar.q2, SlowRed<W>{A},
                       [&](int e) -> uint64_t { return bload(r, vo, LastIO<kBigS>::so(e)); });
-    inv_poly_from_regs<kBigS, NEGA>(lds, v, tau, out + (poly << (kBigS + M)) + o, valid, A,
-                                    MONT ? A.ninv_r : A.ninv, MONT ? A.untwist_r : A.untwist, M, o);
+    inv_poly_from_regs<kBigS>(lds, v, tau, out + (poly << (kBigS + M)) + o, valid, A,
+                                    MONT ? A.ninv_r : A.ninv, M);
 }
 
 // ---------------------------------------------------------------- columns
@@ -166,16 +166,16 @@ __global__ void __launch_bounds__(256) k_big_inv_cols(const uint64_t *__restrict
 }
 
 // ---------------------------------------------------------------- host side
-template <int M, typename W, bool NEGA>
+template <int M, typename W>
 struct Big {
     static hipError_t rows_fwd(const Plan &p, const NttArgs<W> &A, const uint64_t *in, uint64_t *out, size_t nb) {
         const dim3 g(big_blocks(nb, M)), t(Geo<kBigS>::THREADS);
         if constexpr (sizeof(W) == 4)
             if (p.lazy) {
-                hipLaunchKernelGGL((k_big_fwd_rows<M, W, NEGA, true>), g, t, 0, p.stream, in, out, nb, A);
+                hipLaunchKernelGGL((k_big_fwd_rows<M, W, true>), g, t, 0, p.stream, in, out, nb, A);
                 return hipGetLastError();
             }
-        hipLaunchKernelGGL((k_big_fwd_rows<M, W, NEGA, false>), g, t, 0, p.stream, in, out, nb, A);
+        hipLaunchKernelGGL((k_big_fwd_rows<M, W, false>), g, t, 0, p.stream, in, out, nb, A);
         return hipGetLastError();
     }
     template <int EPI>
@@ -193,7 +193,7 @@ struct Big {
     template <bool MONT>
     static hipError_t rows_inv(const Plan &p, const NttArgs<W> &A, const uint64_t *in, uint64_t *out, size_t nb) {
         const dim3 g(big_blocks(nb, M)), t(Geo<kBigS>::THREADS);
-        hipLaunchKernelGGL((k_big_inv_rows<M, W, NEGA, MONT>), g, t, 0, p.stream, in, out, nb, A);
+        hipLaunchKernelGGL((k_big_inv_rows<M, W, MONT>), g, t, 0, p.stream, in, out, nb, A);
         return hipGetLastError();
     }
 
@@ -232,11 +232,11 @@ struct Big {
     }
 };
 
-template <typename W, bool NEGA>
+template <typename W>
 static hipError_t big_dispatch(const Plan &p, const NttArgs<W> &A, int op, const uint64_t *a, const uint64_t *b,
                                uint64_t *c, size_t batch) {
-    if (p.logn == kBigS + 1) return Big<1, W, NEGA>::run(p, A, op, a, b, c, batch);
-    if (p.logn == kBigS + 2) return Big<2, W, NEGA>::run(p, A, op, a, b, c, batch);
+    if (p.logn == kBigS + 1) return Big<1, W>::run(p, A, op, a, b, c, batch);
+    if (p.logn == kBigS + 2) return Big<2, W>::run(p, A, op, a, b, c, batch);
     return hipErrorInvalidValue;
 }
 
@@ -253,11 +253,9 @@ hipError_t launch_big(const Plan &p, int op, const uint64_t *a, const uint64_t *
     else if (bs.last != p.stream) e = hipStreamWaitEvent(p.stream, bs.done, 0);
     if (e != hipSuccess) return e;
     if (p.word == 32)
-        e = p.nega ? big_dispatch<uint32_t, true>(p, p.a32, op, a, b, c, batch)
-                   : big_dispatch<uint32_t, false>(p, p.a32, op, a, b, c, batch);
+        e = big_dispatch<uint32_t>(p, p.a32, op, a, b, c, batch);
     else
-        e = p.nega ? big_dispatch<uint64_t, true>(p, p.a64, op, a, b, c, batch)
-                   : big_dispatch<uint64_t, false>(p, p.a64, op, a, b, c, batch);
+        e = big_dispatch<uint64_t>(p, p.a64, op, a, b, c, batch);
     if (e != hipSuccess) return e;
     e = hipEventRecord(bs.done, p.stream);
     bs.last = p.stream;

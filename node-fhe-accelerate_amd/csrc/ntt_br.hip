@@ -40,7 +40,7 @@ struct BrArgs {
 template <int LOGN>
 constexpr int br_key() { return gk(LOGN, LOGN - 7); }
 
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
     constexpr int K = br_key<LOGN>();
     using G = Geo<K>;
@@ -101,10 +101,6 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
                 if (d > half) d = red_q(q - (base - d), q, mu);
                 return d;
             });
-            if constexpr (NEGA) {
-#pragma unroll
-                for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tr + cbrv(t, G::LOGE) * G::T]);
-            }
             fwd_pass<K, 0, false>(v, t0, A.ar);
             fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
             // raw output (< 4q) times a canonical key: a valid Montgomery pair
@@ -124,7 +120,7 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
         uint32_t ti = tau;
         asm volatile("" : "+v"(ti));
         uint64_t *ap = accs[pl];
-        inv_poly_from_regs<K, NEGA, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, A.untwist, 0, 0,
+        inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
                                                       [&](uint32_t gi, uint64_t x) -> uint64_t {
                                                           ap[gi] = addq(x, red_q(ap[gi], q, mu), q);
                                                           return 0;
@@ -136,17 +132,17 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
 
 bool br_persist_supported(const Plan &p, int k1) { return k1 == 2 && p.logn >= 9 && p.logn <= 11; }
 
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 static hipError_t br_one(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
-    hipLaunchKernelGGL((k_br_persist<LOGN, W, NEGA>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+    hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
     return hipGetLastError();
 }
-template <typename W, bool NEGA>
+template <typename W>
 static hipError_t br_dispatch(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
     switch (p.logn) {
-    case 9: return br_one<9, W, NEGA>(p, D, batch, A);
-    case 10: return br_one<10, W, NEGA>(p, D, batch, A);
-    case 11: return br_one<11, W, NEGA>(p, D, batch, A);
+    case 9: return br_one<9, W>(p, D, batch, A);
+    case 10: return br_one<10, W>(p, D, batch, A);
+    case 11: return br_one<11, W>(p, D, batch, A);
     default: return hipErrorInvalidValue;
     }
 }
@@ -162,10 +158,8 @@ hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uin
         const size_t nb = batch - b0 < per ? batch - b0 : per;
         BrArgs D{acc + b0 * 2 * ((size_t)1 << p.logn), bsk, lwe_a + b0 * lwe_dim, lwe_b + b0, lwe_q, lwe_dim, level,
                  base_log};
-        hipError_t e = p.word == 32 ? (p.nega ? br_dispatch<uint32_t, true>(p, D, nb, p.a32)
-                                              : br_dispatch<uint32_t, false>(p, D, nb, p.a32))
-                                    : (p.nega ? br_dispatch<uint64_t, true>(p, D, nb, p.a64)
-                                              : br_dispatch<uint64_t, false>(p, D, nb, p.a64));
+        hipError_t e = p.word == 32 ? br_dispatch<uint32_t>(p, D, nb, p.a32)
+                                    : br_dispatch<uint64_t>(p, D, nb, p.a64);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -54,7 +54,7 @@ constexpr int ctmul_occ() {
     return Geo<LOGN>::template occ_waves<W, NL * Geo<LOGN>::P * Geo<LOGN>::N>();
 }
 
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ctmul_occ<LOGN, W>()))
 k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *out, size_t batch,
          NttArgs<W> A) {
@@ -134,14 +134,14 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 
     // 1. A = X0
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr, valid, A);
+    fwd_poly<LOGN, LAZY, kPfPolymul>(lds, v, tp, xr, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) st(SA, gidx<LOGN, G::NP - 1>(tp, e), e, fwd_to_canon<LAZY>(v[e], A));
     if constexpr (G::NP > 1) __syncthreads();
 
     // 2. Y0: B = Y0, c0 = inv(X0 Y0)
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr, valid, A, 0, 0, [&] { fetch(SA, 0); });
+    fwd_poly<LOGN, LAZY, kPfPolymul>(lds, v, tp, yr, valid, A, 0, [&] { fetch(SA, 0); });
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
@@ -151,12 +151,12 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     }
     __syncthreads();
     tp = lane();
-    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, kPfPolymul>(lds, v, tp, orow, valid, A, A.ninv_r);
     __syncthreads();
 
     // 3. X1: C = X1 Y0, B = X1
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, xr + G::N, valid, A, 0, 0, [&] { fetch(SB, 1); });
+    fwd_poly<LOGN, LAZY, kPfPolymul>(lds, v, tp, xr + G::N, valid, A, 0, [&] { fetch(SB, 1); });
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tp, e);
@@ -168,7 +168,7 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 
     // 4. Y1: c1 = C + X0 Y1, C = X1 Y1
     tp = lane();
-    fwd_poly<LOGN, NEGA, LAZY, kPfPolymul>(lds, v, tp, yr + G::N, valid, A, 0, 0, [&] {
+    fwd_poly<LOGN, LAZY, kPfPolymul>(lds, v, tp, yr + G::N, valid, A, 0, [&] {
         fetch(SA, 0);
         fetch(SB, 1);
     });
@@ -182,12 +182,12 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     }
     __syncthreads();  // every slot read of rows 1/2 precedes their final stores
     tp = lane();
-    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow + G::N, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, kPfPolymul>(lds, v, tp, orow + G::N, valid, A, A.ninv_r);
     __syncthreads();
     tp = lane();
 #pragma unroll
     for (int e = 0; e < G::E; ++e) v[e] = ld(SC, gidx<LOGN, G::NP - 1>(tp, e), e);
-    inv_poly_from_regs<LOGN, NEGA, kPfPolymul>(lds, v, tp, orow + 2 * G::N, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, kPfPolymul>(lds, v, tp, orow + 2 * G::N, valid, A, A.ninv_r);
 }
 
 // 32 coefficients per thread (q < 2^30, N = 8192 / 16384): two workgroups
@@ -205,7 +205,7 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 #ifndef FHE_CTMUL_E16
 #define FHE_CTMUL_E16 0
 #endif
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *out, size_t batch,
           NttArgs<W> A) {
@@ -221,7 +221,7 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     W *s1 = reinterpret_cast<W *>(orow + G::N), *s2 = reinterpret_cast<W *>(orow + 2 * G::N);
     W a[G::E], b[G::E];
     // 1-2
-    fwd_poly2<LOGN, NEGA, LAZY, PF>(lds, a, b, tau, xr, yr, A);
+    fwd_poly2<LOGN, LAZY, PF>(lds, a, b, tau, xr, yr, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
@@ -233,12 +233,12 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     __syncthreads();
     uint32_t t1 = tau;
     asm volatile("" : "+v"(t1));
-    inv_poly_from_regs<LOGN, NEGA, PF>(lds, a, t1, orow, true, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, PF>(lds, a, t1, orow, true, A, A.ninv_r);
     __syncthreads();
     // 3-4
     uint32_t t2 = tau;
     asm volatile("" : "+v"(t2));
-    fwd_poly2<LOGN, NEGA, LAZY, PF>(lds, a, b, t2, xr + G::N, yr + G::N, A);
+    fwd_poly2<LOGN, LAZY, PF>(lds, a, b, t2, xr + G::N, yr + G::N, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(t2, e);
@@ -252,10 +252,10 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     __syncthreads();  // every stash read precedes the final stores of rows 1 / 2
     uint32_t t3 = tau;
     asm volatile("" : "+v"(t3));
-    inv_poly2<LOGN, NEGA, PF>(lds, a, b, t3, orow + G::N, orow + 2 * G::N, A, A.ninv_r, A.untwist_r);
+    inv_poly2<LOGN, PF>(lds, a, b, t3, orow + G::N, orow + 2 * G::N, A, A.ninv_r);
 }
 
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *x, const uint64_t *y, uint64_t *out,
                             size_t batch) {
     using G = Geo<LOGN>;
@@ -268,31 +268,31 @@ static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *
         constexpr int K = sizeof(W) == 4 ? gk(LOGN, 5) : LOGN;
         if constexpr (sizeof(W) == 4) {
             if (lazy) {
-                hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, true>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y,
+                hipLaunchKernelGGL((k_ct_mul2<K, W, true>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y,
                                    out, batch, A);
                 return hipGetLastError();
             }
         }
-        hipLaunchKernelGGL((k_ct_mul2<K, W, NEGA, false>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y, out,
+        hipLaunchKernelGGL((k_ct_mul2<K, W, false>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y, out,
                            batch, A);
     } else {
         if (lazy) {
             if constexpr (sizeof(W) == 4)
-                hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, true>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y,
+                hipLaunchKernelGGL((k_ct_mul<LOGN, W, true>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y,
                                    out, batch, A);
         } else
-            hipLaunchKernelGGL((k_ct_mul<LOGN, W, NEGA, false>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
+            hipLaunchKernelGGL((k_ct_mul<LOGN, W, false>), dim3(blocks), dim3(G::THREADS), 0, p.stream, x, y, out,
                                batch, A);
     }
     return hipGetLastError();
 }
 
-template <typename W, bool NEGA>
+template <typename W>
 static hipError_t ctmul_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_t *x, const uint64_t *y,
                                  uint64_t *out, size_t batch) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return ctmul_one<L, W, NEGA>(p, A, x, y, out, batch);
+    case L: return ctmul_one<L, W>(p, A, x, y, out, batch);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -303,10 +303,8 @@ static hipError_t ctmul_dispatch(const Plan &p, const NttArgs<W> &A, const uint6
 hipError_t launch_ct_mul(const Plan &p, const uint64_t *x, const uint64_t *y, uint64_t *out, size_t batch) {
     if (batch == 0) return hipSuccess;
     if (p.word == 32)
-        return p.nega ? ctmul_dispatch<uint32_t, true>(p, p.a32, x, y, out, batch)
-                      : ctmul_dispatch<uint32_t, false>(p, p.a32, x, y, out, batch);
-    return p.nega ? ctmul_dispatch<uint64_t, true>(p, p.a64, x, y, out, batch)
-                  : ctmul_dispatch<uint64_t, false>(p, p.a64, x, y, out, batch);
+        return ctmul_dispatch<uint32_t>(p, p.a32, x, y, out, batch);
+    return ctmul_dispatch<uint64_t>(p, p.a64, x, y, out, batch);
 }
 
 }  // namespace FHE_NS

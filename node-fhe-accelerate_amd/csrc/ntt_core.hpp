@@ -3,7 +3,9 @@
 // Transform reproduced (ntt_processor.cpp:262-380):
 //   forward:  bit-reverse, then for stage s = 0..L-1 (m = 2^s), pairs
 //             (k+j, k+j+m) with twiddle psi^(j*N/2m)  (compat mode), or
-//             psi^(j*N/m) after a psi^i pre-twist (negacyclic mode);
+//             psi^((2j+1)*N/2m)  (negacyclic mode: the psi^i pre-twist of a
+//             cyclic transform merged into the stage twiddles -- the same
+//             butterflies, only the stage table differs, fhe_gpu.cpp);
 //   inverse:  Gentleman-Sande stages L-1..0 with psi^-(...), bit-reverse,
 //             scale by N^-1.
 //
@@ -122,6 +124,20 @@ __device__ __forceinline__ uint32_t wg_poly() {
     if constexpr (G::P == 1) return 0u;
     else return threadIdx.x >> G::LOGT;
 }
+
+// Lane index rebuilt on demand from the wave index (an SGPR) and mbcnt, for
+// kernels that need threadIdx.x again after a register-heavy stretch: no
+// VGPR holds it across the stretch (asm volatile: never hoisted or merged).
+// Valid for workgroups of whole waves.
+struct TidSource {
+    uint32_t wave;
+    __device__ TidSource() : wave(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {}
+    __device__ uint32_t operator()() const {
+        uint32_t t;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(t));
+        return (wave << 6) | t;
+    }
+};
 
 __host__ __device__ constexpr uint32_t cbrv(uint32_t x, int bits) {
     uint32_t r = 0;
@@ -680,9 +696,6 @@ template <typename W>
 struct NttArgs {
     const Tw<W> *twf;      // forward stage table
     const Tw<W> *twi;      // inverse stage table
-    const Tw<W> *twist;    // psi^i          (negacyclic pre-twist)
-    const Tw<W> *untwist;  // psi^-i * N^-1  (negacyclic post-twist)
-    const Tw<W> *untwist_r;// psi^-i * N^-1 * R (post-twist after a Montgomery product)
     Arith<W> ar;
     uint64_t q64, mu64;    // exact slow-path reduction of out-of-range inputs
     Tw<W> ninv;            // N^-1
@@ -783,9 +796,7 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
 // each, so only IN chunks of CH are in flight at once and each chunk is
 // narrowed before the next is issued (scheduling barriers keep the compiler
 // from hoisting all 32 loads, which spills beside a parked spectrum).
-// RELOAD = false keeps each chunk's raw words live through the slow path
-// instead (measured: fewer spills when a pre-twist follows the load).
-template <int E, int CH, int IN, bool RELOAD = true, typename W, typename RD, typename F>
+template <int E, int CH, int IN, typename W, typename RD, typename F>
 __device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, RD &&red, F &&addr_of) {
     constexpr int NC = E / CH;
     uint64_t raw[E];
@@ -800,31 +811,16 @@ __device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, RD 
             for (int t = (c + IN) * CH; t < (c + IN) * CH + CH; ++t) raw[t] = addr_of(t);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (RELOAD) {
-            uint32_t bad = 0;
+        uint32_t bad = 0;
 #pragma unroll
-            for (int t = c * CH; t < c * CH + CH; ++t) {
-                bad |= uint32_t(raw[t] >= lim) << (t - c * CH);
-                v[t] = W(raw[t]);
-            }
-            if (__builtin_expect(bad != 0, 0)) {  // reload and reduce (see load_coeffs_r)
+        for (int t = c * CH; t < c * CH + CH; ++t) {
+            bad |= uint32_t(raw[t] >= lim) << (t - c * CH);
+            v[t] = W(raw[t]);
+        }
+        if (__builtin_expect(bad != 0, 0)) {  // reload and reduce (see load_coeffs_r)
 #pragma unroll
-                for (int t = c * CH; t < c * CH + CH; ++t)
-                    if ((bad >> (t - c * CH)) & 1) v[t] = W(red(addr_of(t)));
-            }
-        } else {
-            bool bad = false;
-#pragma unroll
-            for (int t = c * CH; t < c * CH + CH; ++t) bad |= raw[t] >= lim;
-            if (__builtin_expect(bad, 0)) {
-#pragma unroll
-                for (int t = c * CH; t < c * CH + CH; ++t) {
-                    if (raw[t] >= lim) raw[t] = red(raw[t]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-#pragma unroll
-            for (int t = c * CH; t < c * CH + CH; ++t) v[t] = W(raw[t]);
+            for (int t = c * CH; t < c * CH + CH; ++t)
+                if ((bad >> (t - c * CH)) & 1) v[t] = W(red(addr_of(t)));
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -837,9 +833,8 @@ __device__ __forceinline__ void load_coeffs_chunked(W (&v)[E], uint64_t lim, RD 
 // RS: the result is the transform times R (Montgomery form).
 //
 // Sub-transform use (N > 16384, ntt_big.hip): the 2^LOGN coefficients are
-// the strided subsequence src[i << sh] of a larger polynomial whose element
-// src[0] has global index `off` (twist table index (i << sh) | off); the
-// prefix stages of the big transform use the same stage-major twiddles.
+// the strided subsequence src[i << sh] of a larger polynomial; the prefix
+// stages of the big transform use the same stage-major twiddles.
 // Raw pass-0 coefficients of a P == 1 polynomial (bit-reversed order), for
 // prefetching through a fwd_rest hook.
 template <int LOGN>
@@ -849,33 +844,27 @@ __device__ __forceinline__ void load_raw(uint64_t (&raw)[Geo<LOGN>::E], uint32_t
 #pragma unroll
     for (int t = 0; t < G::E; ++t) raw[t] = bload(r, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u);
 }
-template <int LOGN, bool NEGA, bool LAZY, int PF = kPfSingle, bool RS = false, typename W, typename H = NoHook>
+template <int LOGN, bool LAZY, int PF = kPfSingle, bool RS = false, typename W, typename H = NoHook>
 __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const uint64_t *__restrict__ src,
-                                         bool valid, const NttArgs<W> &A, uint32_t sh = 0, uint32_t off = 0,
-                                         H &&hook = NoHook{}, uint64_t (*pre)[Geo<LOGN>::E] = nullptr) {
+                                         bool valid, const NttArgs<W> &A, uint32_t sh = 0, H &&hook = NoHook{}, uint64_t (*pre)[Geo<LOGN>::E] = nullptr) {
     using G = Geo<LOGN>;
     constexpr bool ST = stream_tw<LOGN, W>();
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
     if constexpr (!ST) load_tw<LOGN, 0>(tau, A.twf, t0);
-    // Shoup-based first steps (twist / R-scaling) accept any word
-    const uint64_t lim = (NEGA || RS) ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
+    // a Shoup-based first step (R-scaling) accepts any word
+    const uint64_t lim = RS ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     if (pre) {  // prefetched by the caller (load_raw)
         coeffs_from_raw<G::E>(v, *pre, lim, SlowRed<W>{A});
     } else if constexpr (G::P == 1) {  // the caller has returned early if !valid
         const auto r = brsrc(src);
         const uint32_t vo = (tau << sh) * 8u;
         auto at = [&](int t) -> uint64_t { return bload(r, vo, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u); };
-        if constexpr (G::LOGE == 5) load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT, !NEGA>(v, lim, SlowRed<W>{A}, at);
+        if constexpr (G::LOGE == 5) load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, SlowRed<W>{A}, at);
         else load_coeffs_r<G::E>(v, lim, SlowRed<W>{A}, at);
     } else {
         load_coeffs_r<G::E>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return valid ? __builtin_nontemporal_load(src + ((tau + cbrv(t, G::LOGE) * G::T) << sh)) : 0;
         });
-    }
-    if constexpr (NEGA) {
-#pragma unroll
-        for (int t = 0; t < G::E; ++t)
-            v[t] = A.ar.shoup(v[t], A.twist[((tau + cbrv(t, G::LOGE) * G::T) << sh) | off]);
     }
     if constexpr (ST) {
         stream_begin<LOGN, 0, false, RS>(tau, A.twf, t0);
@@ -888,7 +877,7 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
 
 // fwd_poly for two polynomials at once (P == 1, no sub-transform offsets):
 // results in v (from src) and v2 (from src2), last-pass layout.
-template <int LOGN, bool NEGA, bool LAZY, int PF, typename W>
+template <int LOGN, bool LAZY, int PF, typename W>
 __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
                                           const uint64_t *__restrict__ src, const uint64_t *__restrict__ src2,
                                           const NttArgs<W> &A) {
@@ -897,29 +886,19 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     constexpr bool ST = stream_tw2<LOGN, W>();
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
     if constexpr (!ST) load_tw<LOGN, 0>(tau, A.twf, t0);
-    const uint64_t lim = NEGA ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
+    const uint64_t lim = (uint64_t)(A.ar.q2 * 2);
     const uint32_t vo = tau * 8u;
     {
         const auto r = brsrc(src);
-        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT, !NEGA>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
+        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
         });
     }
     {
         const auto r = brsrc(src2);
-        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT, !NEGA>(v2, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
+        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v2, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
         });
-    }
-    if constexpr (NEGA) {
-#pragma unroll
-        for (int t = 0; t < G::E; ++t) {
-            const Tw<W> tw = A.twist[tau + cbrv(t, G::LOGE) * G::T];
-            v[t] = A.ar.shoup(v[t], tw);
-            v2[t] = A.ar.shoup(v2[t], tw);
-            // u64: 4 twist pairs in flight at a time (16 hoisted = 64 VGPRs)
-            if (sizeof(W) == 8 && (t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
     }
     if constexpr (ST) {
         stream_begin<LOGN, 0, false, false>(tau, A.twf, t0);
@@ -933,19 +912,17 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
 
 // Inverse transform from v (last-pass layout, values in [0, 2q)) to HBM
 // (bit-reversed store, coalesced), canonical output.  scale = N^-1 or
-// N^-1 * R; post = the matching negacyclic post-twist table.
-// Sub-transform use (ntt_big.hip): output i goes to dst[i << sh], global
-// index (i << sh) | off for the post-twist.
+// N^-1 * R, folded into the last stage.
+// Sub-transform use (ntt_big.hip): output i goes to dst[i << sh].
 // fin(gi, x): final map of canonical output x at global index gi (an
 // epilogue fused into the store, e.g. "+ c0" of a relinearisation).
 struct NoFin {
     __device__ uint64_t operator()(uint32_t, uint64_t x) const { return x; }
 };
 // STORE = false: fin() does every store itself (dst unused).
-template <int LOGN, bool NEGA, int PF = kPfSingle, bool STORE = true, typename W, typename F = NoFin>
+template <int LOGN, int PF = kPfSingle, bool STORE = true, typename W, typename F = NoFin>
 __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, uint64_t *__restrict__ dst,
-                                                   bool valid, const NttArgs<W> &A, Tw<W> scale,
-                                                   const Tw<W> *__restrict__ post, uint32_t sh = 0, uint32_t off = 0,
+                                                   bool valid, const NttArgs<W> &A, Tw<W> scale, uint32_t sh = 0,
                                                    F &&fin = NoFin{}) {
     using G = Geo<LOGN>;
     constexpr int LAST = G::NP - 1;
@@ -953,19 +930,17 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
         Tw<W> t[PassTw<LOGN, LAST>::COUNT];
         if constexpr (stream_tw<LOGN, W>()) {
             stream_begin<LOGN, LAST, true, false>(tau, A.twi, t);
-            inv_pass_stream<LOGN, LAST, !NEGA>(tau, v, t, A.twi, A.ar, scale);
+            inv_pass_stream<LOGN, LAST, true>(tau, v, t, A.twi, A.ar, scale);
         } else {
             load_tw<LOGN, LAST>(tau, A.twi, t);
-            inv_pass<LOGN, LAST, !NEGA>(v, t, A.ar, scale);
+            inv_pass<LOGN, LAST, true>(v, t, A.ar, scale);
         }
     }
-    inv_rest<LOGN, LAST - 1, !NEGA, PF>(lds, v, tau, A.twi, A.ar, scale);
+    inv_rest<LOGN, LAST - 1, true, PF>(lds, v, tau, A.twi, A.ar, scale);
 #pragma unroll
     for (int t = 0; t < G::E; ++t) {
         const uint32_t gi = (tau + cbrv(t, G::LOGE) * G::T) << sh;
-        W x = v[t];
-        if constexpr (NEGA) x = A.ar.shoup(x, post[gi | off]);
-        const uint64_t y = fin(gi, (uint64_t)A.ar.red1q(x));
+        const uint64_t y = fin(gi, (uint64_t)A.ar.red1q(v[t]));
         if constexpr (!STORE) (void)y;
         else if constexpr (G::P == 1)
             bstore(brsrc(dst), (tau << sh) * 8u, ((cbrv(t, G::LOGE) * G::T) << sh) * 8u, y);
@@ -1014,11 +989,10 @@ __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);
     }
 }
-template <int LOGN, bool NEGA, int PF, typename W, typename F1 = NoFin, typename F2 = NoFin>
+template <int LOGN, int PF, typename W, typename F1 = NoFin, typename F2 = NoFin>
 __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
                                           uint64_t *__restrict__ dst, uint64_t *__restrict__ dst2,
-                                          const NttArgs<W> &A, Tw<W> scale, const Tw<W> *__restrict__ post,
-                                          F1 &&fin1 = NoFin{}, F2 &&fin2 = NoFin{}) {
+                                          const NttArgs<W> &A, Tw<W> scale, F1 &&fin1 = NoFin{}, F2 &&fin2 = NoFin{}) {
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
     constexpr int LAST = G::NP - 1;
@@ -1026,27 +1000,21 @@ __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         Tw<W> t[PassTw<LOGN, LAST>::COUNT];
         if constexpr (stream_tw2<LOGN, W>()) {
             stream_begin<LOGN, LAST, true, false>(tau, A.twi, t);
-            inv_pass_stream<LOGN, LAST, !NEGA, true>(tau, v, t, A.twi, A.ar, scale, &v2);
+            inv_pass_stream<LOGN, LAST, true, true>(tau, v, t, A.twi, A.ar, scale, &v2);
         } else {
             constexpr int R = PassTw<LOGN, LAST>::R;
             constexpr int KS = R - PF < 0 ? 0 : R - PF;
             load_tw<LOGN, LAST, W, KS, 8>(tau, A.twi, t);
-            inv_stages2<LOGN, LAST, R - 1, R - KS, !NEGA>(tau, v, v2, t, A.twi, A.ar, scale);
+            inv_stages2<LOGN, LAST, R - 1, R - KS, true>(tau, v, v2, t, A.twi, A.ar, scale);
         }
     }
-    inv_rest2<LOGN, LAST - 1, !NEGA, PF>(lds, v, v2, tau, A.twi, A.ar, scale);
+    inv_rest2<LOGN, LAST - 1, true, PF>(lds, v, v2, tau, A.twi, A.ar, scale);
     const auto r1 = brsrc(dst), r2 = brsrc(dst2);
 #pragma unroll
     for (int t = 0; t < G::E; ++t) {
         const uint32_t gi = tau + cbrv(t, G::LOGE) * G::T;
-        W x = v[t], x2 = v2[t];
-        if constexpr (NEGA) {
-            x = A.ar.shoup(x, post[gi]);
-            x2 = A.ar.shoup(x2, post[gi]);
-        }
-        bstore(r1, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin1(gi, (uint64_t)A.ar.red1q(x)));
-        bstore(r2, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin2(gi, (uint64_t)A.ar.red1q(x2)));
-        if (NEGA && sizeof(W) == 8 && (t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        bstore(r1, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin1(gi, (uint64_t)A.ar.red1q(v[t])));
+        bstore(r2, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, fin2(gi, (uint64_t)A.ar.red1q(v2[t])));
     }
 }
 

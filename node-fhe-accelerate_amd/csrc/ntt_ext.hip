@@ -90,7 +90,7 @@ struct DmArgs {
     const uint64_t *src2;   // MODE 3: ct1 [batch][K1][N] (src = ct0)
 };
 
-template <int LOGN, typename W, bool NEGA, int K1, bool LAZY, int MODE>
+template <int LOGN, typename W, int K1, bool LAZY, int MODE>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ext_occ<LOGN, W, K1, MODE>()))
 k_dmac(DmArgs D, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -161,10 +161,6 @@ k_dmac(DmArgs D, NttArgs<W> A) {
             }
             return d;
         });
-        if constexpr (NEGA) {
-#pragma unroll
-            for (int t = 0; t < G::E; ++t) v[t] = A.ar.shoup(v[t], A.twist[tr + cbrv(t, G::LOGE) * G::T]);
-        }
         fwd_pass<LOGN, 0, LAZY>(v, t0, A.ar);
         fwd_rest<LOGN, 1, LAZY, kPfSingle>(lds, v, tr, A.twf, A.ar);
         if (!valid) continue;
@@ -223,7 +219,7 @@ k_dmac(DmArgs D, NttArgs<W> A) {
                 return addq(x, red_q(a, q, mu), q);
             }
         };
-        inv_poly_from_regs<LOGN, NEGA>(lds, v, tr, orow + (size_t)j * G::N, valid, A, A.ninv, A.untwist, 0, 0, fin);
+        inv_poly_from_regs<LOGN>(lds, v, tr, orow + (size_t)j * G::N, valid, A, A.ninv, 0, fin);
     };
     if constexpr (STASH == 3) {  // unrolled: racc is indexed by the row
 #pragma unroll
@@ -246,14 +242,15 @@ k_dmac(DmArgs D, NttArgs<W> A) {
 #ifndef FHE_EXT2
 #define FHE_EXT2 1
 #endif
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_extprod2(DmArgs D, NttArgs<W> A) {
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "one ciphertext per workgroup");
     constexpr int PF = FHE_EXT2_PF;
     __shared__ W lds[G::LW];
-    const uint32_t tau = threadIdx.x;
+    const TidSource tid;  // lane index per phase, not held across phases
+    const uint32_t tau = tid();
     const size_t poly = blockIdx.x;
     if (poly >= D.batch) return;
     const uint64_t *srow = D.src + poly * 2 * G::N;
@@ -271,27 +268,20 @@ k_extprod2(DmArgs D, NttArgs<W> A) {
     };
     load_coeffs<G::E>(v0, lim, q, mu, [&](int t) { return digit(srow, t); });
     load_coeffs<G::E>(v1, lim, q, mu, [&](int t) { return digit(srow + G::N, t); });
-    if constexpr (NEGA) {
-#pragma unroll
-        for (int t = 0; t < G::E; ++t) {
-            const Tw<W> tw = A.twist[tau + cbrv(t, G::LOGE) * G::T];
-            v0[t] = A.ar.shoup(v0[t], tw);
-            v1[t] = A.ar.shoup(v1[t], tw);
-        }
-    }
     fwd_pass<LOGN, 0, false>(v0, t0, A.ar);
     fwd_pass<LOGN, 0, false>(v1, t0, A.ar);
     fwd_rest2<LOGN, 1, false, PF>(lds, v0, v1, tau, A.twf, A.ar);
     // (o0, o1) = (X0 G00 + X1 G10, X0 G01 + X1 G11); raw outputs (< 4q) times
     // canonical prepared keys: valid Montgomery pairs
     const uint64_t *g = D.key;
+    const uint32_t tm = tid();
 #pragma unroll
     for (int e0 = 0; e0 < G::E; e0 += 2) {
         uint64_t k[2][4];
 #pragma unroll
         for (int e = 0; e < 2; ++e)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) k[e][j] = g[(size_t)j * G::N + gidx<LOGN, G::NP - 1>(tau, e0 + e)];
+            for (int j = 0; j < 4; ++j) k[e][j] = g[(size_t)j * G::N + gidx<LOGN, G::NP - 1>(tm, e0 + e)];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const W x0 = v0[e0 + e], x1 = v1[e0 + e];
@@ -300,31 +290,35 @@ k_extprod2(DmArgs D, NttArgs<W> A) {
         }
     }
     __syncthreads();
-    uint32_t ti = tau;
-    asm volatile("" : "+v"(ti));
-    inv_poly2<LOGN, NEGA, PF>(lds, v0, v1, ti, orow, orow + G::N, A, A.ninv, A.untwist);
+    const uint32_t ti = tid();
+    inv_poly2<LOGN, PF>(lds, v0, v1, ti, orow, orow + G::N, A, A.ninv);
 }
 
-template <int LOGN, typename W, bool NEGA, int MODE>
+// FHE_EXT_ACC=0: multi-level external products at N = 16384 take k_dmac
+// (lab A/B against ntt_ext2.hip).
+#ifndef FHE_EXT_ACC
+#define FHE_EXT_ACC 1
+#endif
+template <int LOGN, typename W, int MODE>
 static hipError_t dmac_one(const NttArgs<W> &A, hipStream_t s, int k1, const DmArgs &D) {
     using G = Geo<LOGN>;
     const size_t blocks = (D.batch + G::P - 1) / G::P;
     if (k1 != 2) return hipErrorInvalidValue;
     if constexpr (MODE == 0 && G::P == 1 && FHE_EXT2 && sizeof(W) == 8 && LOGN >= 12) {
         if (D.level == 1) {
-            hipLaunchKernelGGL((k_extprod2<LOGN, W, NEGA>), dim3((unsigned)D.batch), dim3(G::THREADS), 0, s, D, A);
+            hipLaunchKernelGGL((k_extprod2<LOGN, W>), dim3((unsigned)D.batch), dim3(G::THREADS), 0, s, D, A);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((k_dmac<LOGN, W, NEGA, 2, false, MODE>), dim3(blocks), dim3(G::THREADS), 0, s, D, A);
+    hipLaunchKernelGGL((k_dmac<LOGN, W, 2, false, MODE>), dim3(blocks), dim3(G::THREADS), 0, s, D, A);
     return hipGetLastError();
 }
 
-template <typename W, bool NEGA, int MODE>
+template <typename W, int MODE>
 static hipError_t dmac_dispatch(const Plan &p, const NttArgs<W> &A, int k1, const DmArgs &D) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return dmac_one<L, W, NEGA, MODE>(A, p.stream, k1, D);
+    case L: return dmac_one<L, W, MODE>(A, p.stream, k1, D);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -336,14 +330,14 @@ template <int MODE>
 static hipError_t dmac(const Plan &p, int k1, const DmArgs &D) {
     if (D.batch == 0) return hipSuccess;
     if (p.word == 32)
-        return p.nega ? dmac_dispatch<uint32_t, true, MODE>(p, p.a32, k1, D)
-                      : dmac_dispatch<uint32_t, false, MODE>(p, p.a32, k1, D);
-    return p.nega ? dmac_dispatch<uint64_t, true, MODE>(p, p.a64, k1, D)
-                  : dmac_dispatch<uint64_t, false, MODE>(p, p.a64, k1, D);
+        return dmac_dispatch<uint32_t, MODE>(p, p.a32, k1, D);
+    return dmac_dispatch<uint64_t, MODE>(p, p.a64, k1, D);
 }
 
 hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const uint64_t *glwe,
                           const uint64_t *ggsw, uint64_t *out, size_t batch) {
+    if (FHE_EXT_ACC && extprod_acc_supported(p, k1, level, base_log))
+        return launch_extprod_acc(p, level, base_log, glwe, ggsw, out, batch);
     DmArgs D{glwe, ggsw, out, batch, level, base_log, nullptr, 0, 0, 0, nullptr};
     return dmac<0>(p, k1, D);
 }

@@ -20,7 +20,7 @@
 
 namespace FHE_NS {
 
-template <int LOGN, typename W, bool NEGA, bool LAZY, int EPI>
+template <int LOGN, typename W, bool LAZY, int EPI>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -32,7 +32,7 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
     if (G::P == 1 && !valid) return;  // whole workgroup: no barrier is skipped
     W v[G::E];
     // EPI 1: transform times R (Montgomery form), folded into stage 0
-    fwd_poly<LOGN, NEGA, LAZY, kPfSingle, EPI == 1>(lds, v, tau, in + poly * G::N, valid, A);
+    fwd_poly<LOGN, LAZY, kPfSingle, EPI == 1>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     uint64_t *dst = out + poly * G::N;
     if constexpr (G::P == 1) {
@@ -52,7 +52,7 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 #ifndef FHE_FWDMUL_PREFETCH
 #define FHE_FWDMUL_PREFETCH 1
 #endif
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
               size_t batch, NttArgs<W> A) {
@@ -79,7 +79,7 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
 #pragma unroll
             for (int e = 0; e < G::E; ++e) rw[e] = bload(r, vo, LastIO<LOGN>::so(e));
         };
-        fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A, 0, 0, hook);
+        fwd_poly<LOGN, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A, 0, hook);
         W w[G::E];
         coeffs_from_raw<G::E>(w, rw, A.q64, SlowRed<W>{A});
         const auto ro = brsrc(dst);
@@ -88,7 +88,7 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
         return;
     }
 #endif
-    fwd_poly<LOGN, NEGA, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A);
+    fwd_poly<LOGN, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A);
     if (!valid) return;
     // two chunks: 16 raw u64 w in flight at once would exceed 64 VGPRs
     constexpr int CH = G::E >= 8 ? G::E / 8 : G::E;
@@ -125,35 +125,35 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
 template <int LOGN, typename W>
 constexpr int fwd_key() { return (FHE_FWD64_E32 && sizeof(W) == 8 && LOGN == 14) ? gk(LOGN, 5) : LOGN; }
 
-template <int LOGN0, typename W, bool NEGA, bool LAZY>
+template <int LOGN0, typename W, bool LAZY>
 static hipError_t fwd_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *in, uint64_t *out, size_t batch,
                           int epi, const uint64_t *wv) {
     constexpr int LOGN = fwd_key<LOGN0, W>();
     using G = Geo<LOGN>;
     const size_t blocks = (batch + G::P - 1) / G::P;
     if (wv)
-        hipLaunchKernelGGL((k_ntt_fwd_mul<LOGN, W, NEGA, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, in, wv, out,
+        hipLaunchKernelGGL((k_ntt_fwd_mul<LOGN, W, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, in, wv, out,
                            batch, A);
     else if (epi == 1)
-        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, LAZY, 1>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, LAZY, 1>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
     else
-        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, NEGA, LAZY, 0>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN, W, LAZY, 0>), dim3(blocks), dim3(G::THREADS), 0, s, in, out, batch, A);
     return hipGetLastError();
 }
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 static hipError_t fwd_lazy(const Plan &p, const NttArgs<W> &A, const uint64_t *in, uint64_t *out, size_t batch,
                            int epi, const uint64_t *wv) {
     if constexpr (sizeof(W) == 4)
-        if (p.lazy) return fwd_one<LOGN, W, NEGA, true>(A, p.stream, in, out, batch, epi, wv);
-    return fwd_one<LOGN, W, NEGA, false>(A, p.stream, in, out, batch, epi, wv);
+        if (p.lazy) return fwd_one<LOGN, W, true>(A, p.stream, in, out, batch, epi, wv);
+    return fwd_one<LOGN, W, false>(A, p.stream, in, out, batch, epi, wv);
 }
 
-template <typename W, bool NEGA>
+template <typename W>
 static hipError_t fwd_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_t *in, uint64_t *out, size_t batch,
                                int epi, const uint64_t *wv) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return fwd_lazy<L, W, NEGA>(p, A, in, out, batch, epi, wv);
+    case L: return fwd_lazy<L, W>(p, A, in, out, batch, epi, wv);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -165,10 +165,8 @@ static hipError_t fwd_any(const Plan &p, const uint64_t *in, uint64_t *out, size
                           const uint64_t *wv) {
     if (batch == 0) return hipSuccess;
     if (p.word == 32)
-        return p.nega ? fwd_dispatch<uint32_t, true>(p, p.a32, in, out, batch, epi, wv)
-                      : fwd_dispatch<uint32_t, false>(p, p.a32, in, out, batch, epi, wv);
-    return p.nega ? fwd_dispatch<uint64_t, true>(p, p.a64, in, out, batch, epi, wv)
-                  : fwd_dispatch<uint64_t, false>(p, p.a64, in, out, batch, epi, wv);
+        return fwd_dispatch<uint32_t>(p, p.a32, in, out, batch, epi, wv);
+    return fwd_dispatch<uint64_t>(p, p.a64, in, out, batch, epi, wv);
 }
 
 hipError_t launch_fwd(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch, int epi) {

@@ -11,7 +11,7 @@
 
 namespace FHE_NS {
 
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
     using G = Geo<LOGN>;
@@ -35,7 +35,7 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
             v[e] = load_lazy<W>(x, lim, A.q64, A.mu64);
         }
     }
-    inv_poly_from_regs<LOGN, NEGA>(lds, v, tau, out + poly * G::N, valid, A, A.ninv, A.untwist);
+    inv_poly_from_regs<LOGN>(lds, v, tau, out + poly * G::N, valid, A, A.ninv);
 }
 
 // Where fwd(a) waits while fwd(b) runs: 0 = VGPRs (small N), 1 = a second
@@ -122,7 +122,7 @@ constexpr bool polymul_dual() {
 template <int LOGN, typename W>
 constexpr int polymul2_pf() { return sizeof(W) == 8 ? FHE_PF_DUAL64 : polymul_pf<LOGN>(); }
 
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
 k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
           NttArgs<W> A) {
@@ -146,7 +146,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     auto hook = [&] {
         if constexpr (PRE) load_raw<LOGN>(*reinterpret_cast<uint64_t(*)[G::E]>(rb), tau, b + poly * G::N);
     };
-    fwd_poly<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, tau, a + poly * G::N, valid, A, 0, 0, hook);
+    fwd_poly<LOGN, LAZY, polymul_pf<LOGN>()>(lds, v, tau, a + poly * G::N, valid, A, 0, hook);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const W x = fwd_to_canon<LAZY>(v[e], A);  // canonical: times a raw output below
@@ -166,10 +166,10 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     uint32_t tb = tau;
     if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(tb));
     if constexpr (PRE)
-        fwd_poly<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, tb, b + poly * G::N, valid, A, 0, 0, NoHook{},
+        fwd_poly<LOGN, LAZY, polymul_pf<LOGN>()>(lds, v, tb, b + poly * G::N, valid, A, 0, NoHook{},
                                                reinterpret_cast<uint64_t(*)[G::E]>(rb));
     else
-        fwd_poly<LOGN, NEGA, LAZY, polymul_pf<LOGN>()>(lds, v, tb, b + poly * G::N, valid, A);
+        fwd_poly<LOGN, LAZY, polymul_pf<LOGN>()>(lds, v, tb, b + poly * G::N, valid, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tb, e);
@@ -182,7 +182,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     if constexpr (G::NP > 1) __syncthreads();
     uint32_t ti = tau;
     if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(ti));
-    inv_poly_from_regs<LOGN, NEGA, polymul_pf<LOGN>()>(lds, v, ti, crow, valid, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, polymul_pf<LOGN>()>(lds, v, ti, crow, valid, A, A.ninv_r);
 }
 
 // Polymul with 32 coefficients per thread: fwd(a) and fwd(b) run in
@@ -190,7 +190,7 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
 // then the pointwise Montgomery product and the inverse.  Two workgroups per
 // CU (one 64 KiB exchange buffer each), so one's HBM traffic overlaps the
 // other's transforms.
-template <int LOGN, typename W, bool NEGA, bool LAZY>
+template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
            NttArgs<W> A) {
@@ -201,14 +201,14 @@ k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint6
     const size_t poly = blockIdx.x;
     if (poly >= batch) return;
     W v[G::E], vb[G::E];
-    fwd_poly2<LOGN, NEGA, LAZY, polymul2_pf<LOGN, W>()>(lds, v, vb, tau, a + poly * G::N, b + poly * G::N, A);
+    fwd_poly2<LOGN, LAZY, polymul2_pf<LOGN, W>()>(lds, v, vb, tau, a + poly * G::N, b + poly * G::N, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) v[e] = A.ar.mont(fwd_to_canon<LAZY>(v[e], A), vb[e]);  // canonical x raw (< R)
     __syncthreads();  // the exchange buffer still holds b's last layout reads
-    inv_poly_from_regs<LOGN, NEGA, polymul2_pf<LOGN, W>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r, A.untwist_r);
+    inv_poly_from_regs<LOGN, polymul2_pf<LOGN, W>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r);
 }
 
-template <int LOGN, typename W, bool NEGA>
+template <int LOGN, typename W>
 static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, const uint64_t *a, const uint64_t *b,
                           uint64_t *c, size_t batch) {
     bool lazy = false;
@@ -220,21 +220,21 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
         if (b) {
             if constexpr (sizeof(W) == 4) {
                 if (lazy) {
-                    hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b,
+                    hipLaunchKernelGGL((k_polymul2<PK, W, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b,
                                        c, batch, A);
                     return hipGetLastError();
                 }
             }
-                hipLaunchKernelGGL((k_polymul2<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+                hipLaunchKernelGGL((k_polymul2<PK, W, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
             return hipGetLastError();
         }
     } else {
         if (b && lazy) {
             if constexpr (sizeof(W) == 4)
-                hipLaunchKernelGGL((k_polymul<PK, W, NEGA, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+                hipLaunchKernelGGL((k_polymul<PK, W, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
             return hipGetLastError();
         } else if (b) {
-            hipLaunchKernelGGL((k_polymul<PK, W, NEGA, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
+            hipLaunchKernelGGL((k_polymul<PK, W, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
             return hipGetLastError();
         }
     }
@@ -242,17 +242,17 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
         constexpr int IK = inv_key<LOGN, W>();
         using GI = Geo<IK>;
         const size_t iblocks = (batch + GI::P - 1) / GI::P;
-        hipLaunchKernelGGL((k_ntt_inv<IK, W, NEGA>), dim3(iblocks), dim3(GI::THREADS), 0, s, a, c, batch, A);
+        hipLaunchKernelGGL((k_ntt_inv<IK, W>), dim3(iblocks), dim3(GI::THREADS), 0, s, a, c, batch, A);
     }
     return hipGetLastError();
 }
 
-template <typename W, bool NEGA>
+template <typename W>
 static hipError_t inv_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_t *a, const uint64_t *b,
                                uint64_t *c, size_t batch) {
     switch (p.logn) {
 #define FHE_CASE(L) \
-    case L: return inv_one<L, W, NEGA>(p, A, p.stream, a, b, c, batch);
+    case L: return inv_one<L, W>(p, A, p.stream, a, b, c, batch);
         FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
         FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
 #undef FHE_CASE
@@ -263,10 +263,8 @@ static hipError_t inv_dispatch(const Plan &p, const NttArgs<W> &A, const uint64_
 static hipError_t inv_any(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch) {
     if (batch == 0) return hipSuccess;
     if (p.word == 32)
-        return p.nega ? inv_dispatch<uint32_t, true>(p, p.a32, a, b, c, batch)
-                      : inv_dispatch<uint32_t, false>(p, p.a32, a, b, c, batch);
-    return p.nega ? inv_dispatch<uint64_t, true>(p, p.a64, a, b, c, batch)
-                  : inv_dispatch<uint64_t, false>(p, p.a64, a, b, c, batch);
+        return inv_dispatch<uint32_t>(p, p.a32, a, b, c, batch);
+    return inv_dispatch<uint64_t>(p, p.a64, a, b, c, batch);
 }
 
 hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch) {
