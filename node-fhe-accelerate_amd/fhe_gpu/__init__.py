@@ -325,6 +325,30 @@ def find_primitive_root(degree: int, modulus: int) -> int:  # :92-128
 
 
 # ----------------------------------------------------------------- NTT / ring
+def env_defaults(mode=None, device=None, devices=None):
+    """Context defaults from the environment (SURVEY.md section 5 config flags):
+    FHE_NTT_MODE = compat | negacyclic (mode when not given);
+    FHE_GPU_DEVICES = comma-separated GPU ordinals (device list when neither
+    device nor devices is given: one entry -> that device, several -> a
+    multi-device context).  Returns (mode, device, devices)."""
+    if mode is None:
+        mode = os.environ.get("FHE_NTT_MODE", "compat").strip() or "compat"
+    if device is None and devices is None:
+        env = os.environ.get("FHE_GPU_DEVICES", "").strip()
+        if env:
+            try:
+                devs = [int(x) for x in env.split(",") if x.strip()]
+            except ValueError:
+                raise FHEError(-9, f"FHE_GPU_DEVICES must be a comma-separated list of ordinals, got {env!r}")
+            if len(devs) == 1:
+                device = devs[0]
+            elif devs:
+                devices = devs
+    if device is None:
+        device = int(devices[0]) if devices else 0
+    return mode, device, devices
+
+
 class NTTProcessor:
     """NTTProcessor(degree, modulus) on the MI355X (ntt_processor.h:49-306).
 
@@ -340,10 +364,13 @@ class NTTProcessor:
     mod_inverse = staticmethod(mod_inverse)
     find_primitive_root = staticmethod(find_primitive_root)
 
-    def __init__(self, degree: int, modulus: int, mode: str = "compat", device: int = 0, devices=None):
+    def __init__(self, degree: int, modulus: int, mode: str = None, device: int = None, devices=None):
         """devices: a list of GPU ordinals for a multi-device context
         (fhe_ctx_create_multi): host-array batches are split across them, a
-        device tensor runs on the GPU that holds it."""
+        device tensor runs on the GPU that holds it.  Unset arguments come
+        from the environment (env_defaults): mode from FHE_NTT_MODE, the
+        device list from FHE_GPU_DEVICES; otherwise compat on device 0."""
+        mode, device, devices = env_defaults(mode, device, devices)
         m = {"compat": MODE_COMPAT, "negacyclic": MODE_NEGACYCLIC}.get(mode)
         if m is None:
             raise FHEError(-9, f"unknown mode {mode!r}")
@@ -486,7 +513,8 @@ class RNSPolynomialRing:
     [len(moduli), ..., n]; every operation applies to every limb (the
     reference's ring operations use moduli_[0] only)."""
 
-    def __init__(self, degree: int, moduli, mode: str = "compat", device: int = 0):
+    def __init__(self, degree: int, moduli, mode: str = None, device: int = None):
+        mode, device, devs = env_defaults(mode, device, None)  # one device: the first of FHE_GPU_DEVICES
         m = {"compat": MODE_COMPAT, "negacyclic": MODE_NEGACYCLIC}.get(mode)
         if m is None:
             raise FHEError(-9, f"unknown mode {mode!r}")

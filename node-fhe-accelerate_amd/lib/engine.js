@@ -192,10 +192,16 @@ function makeEngineClass(native) {
       // the C++ engines' error std (encryption.cpp:52-56: lwe_noise_std or 3.2)
       this._std = params.lweNoiseStd > 0 ? params.lweNoiseStd : 3.2;
       this._initialBudget = Math.log2(Number(this._q)) - Math.log2(2 * this._std * Math.sqrt(this._n));
-      const mode = o.mode === 'negacyclic' ? 1 : o.mode === undefined || o.mode === 'compat' ? 0 : -1;
-      if (mode < 0) throw new FHEError(`unknown mode ${o.mode}`, FHEErrorCode.INVALID_PARAMETERS);
+      let env;
+      try {
+        env = envDefaults(o);
+      } catch (err) {
+        throw new FHEError(err.message, FHEErrorCode.INVALID_PARAMETERS);
+      }
+      const mode = env.mode === 'negacyclic' ? 1 : env.mode === 'compat' ? 0 : -1;
+      if (mode < 0) throw new FHEError(`unknown mode ${env.mode}`, FHEErrorCode.INVALID_PARAMETERS);
       this._mode = mode;
-      this._ctx = new NttContext(this._n, this._q, mode, o.devices || o.device || 0);
+      this._ctx = new NttContext(this._n, this._q, mode, env.devices || env.device);
       let seed = o.seed;
       if (seed === undefined) seed = crypto.randomBytes(32);
       if (typeof seed === 'bigint' || typeof seed === 'number') {
@@ -839,7 +845,27 @@ function makeEngineClass(native) {
   return { FHEEngineImpl, createEngine };
 }
 
+/**
+ * Context defaults from the environment (SURVEY.md section 5 config flags):
+ * FHE_NTT_MODE = compat | negacyclic when no mode is given; FHE_GPU_DEVICES
+ * = comma-separated GPU ordinals when neither device nor devices is given
+ * (one entry: that device; several: a multi-device context).
+ */
+function envDefaults({ mode, device, devices } = {}) {
+  if (mode === undefined) mode = (process.env.FHE_NTT_MODE || 'compat').trim() || 'compat';
+  if (device === undefined && devices === undefined && process.env.FHE_GPU_DEVICES) {
+    const list = process.env.FHE_GPU_DEVICES.split(',').filter((x) => x.trim() !== '').map(Number);
+    if (list.some((d) => !Number.isInteger(d) || d < 0)) {
+      throw new RangeError(`FHE_GPU_DEVICES must be a comma-separated list of ordinals, got ${process.env.FHE_GPU_DEVICES}`);
+    }
+    if (list.length === 1) device = list[0];
+    else if (list.length > 1) devices = list;
+  }
+  if (device === undefined) device = devices ? devices[0] : 0;
+  return { mode, device, devices };
+}
+
 module.exports = {
-  FHEError, FHEErrorCode, NTT_PRIMES, calculateDerivedParameters, createParameterSet, getAvailablePresets,
+  envDefaults, FHEError, FHEErrorCode, NTT_PRIMES, calculateDerivedParameters, createParameterSet, getAvailablePresets,
   makeEngineClass, toFHEError,
 };

@@ -10,6 +10,7 @@
 const path = require('path');
 
 const native = require(process.env.FHE_NAPI_PATH || path.join(__dirname, '..', 'build', 'fhe_napi.node'));
+const { envDefaults } = require('./engine');
 
 /**
  * Batched polynomial arithmetic over Z_q[X] for the TS FHEEngine
@@ -17,7 +18,8 @@ const native = require(process.env.FHE_NAPI_PATH || path.join(__dirname, '..', '
  * batch * degree coefficients (the reference Polynomial layout).
  */
 class PolynomialEngine {
-  constructor(degree, modulus, { mode = 'compat', device = 0 } = {}) {
+  constructor(degree, modulus, opts = {}) {
+    const { mode, device } = envDefaults(opts);
     const m = mode === 'negacyclic' ? 1 : mode === 'compat' ? 0 : -1;
     if (m < 0) throw new RangeError(`unknown mode ${mode}`);
     this.ctx = new native.NttContext(degree, BigInt(modulus), m, device);
@@ -125,7 +127,8 @@ function gaussian(q, std, count) {
  * the reference's TS control plane (out of scope for this backend).
  */
 class GpuFHEEngine {
-  constructor(params, { mode = 'compat', device = 0, devices } = {}) {
+  constructor(params, opts = {}) {
+    const { mode, device, devices } = envDefaults(opts);
     this.params = params;
     this.n = params.polyDegree;
     this.q = BigInt(params.moduli[0]);

@@ -17,7 +17,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# ORACLE_LIB: an alternative build of ref_cpu.c (the ASan/UBSan build of
+# `make -C oracle sanitize`, loaded by tests/test_sanitize.py)
+_LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 u64p = C.POINTER(C.c_uint64)
@@ -30,9 +32,9 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+        if "ORACLE_LIB" not in os.environ and (not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
             os.path.join(_HERE, "ref_cpu.c")
-        ):
+        )):
             build()
         L = C.CDLL(_LIB_PATH)
         L.oracle_strerror.restype = C.c_char_p

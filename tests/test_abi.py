@@ -204,3 +204,48 @@ def test_kernel_scratch_budget():
             assert k["scratch"] == 0 and k["vgpr_spill"] == 0, (n, k["scratch"], k["vgpr_spill"])
     with_scratch = [n for n, k in zip(names, ks) if k["scratch"]]
     assert len(with_scratch) <= SCRATCH_CEILING, with_scratch
+
+
+# ------------------------------------------------------------ config flags
+def test_env_defaults_python(monkeypatch):
+    """FHE_NTT_MODE / FHE_GPU_DEVICES fill the context
+    arguments a caller leaves unset; explicit arguments win."""
+    import fhe_gpu as fg
+
+    monkeypatch.delenv("FHE_NTT_MODE", raising=False)
+    monkeypatch.delenv("FHE_GPU_DEVICES", raising=False)
+    assert fg.env_defaults() == ("compat", 0, None)
+    monkeypatch.setenv("FHE_NTT_MODE", "negacyclic")
+    monkeypatch.setenv("FHE_GPU_DEVICES", "2")
+    assert fg.env_defaults() == ("negacyclic", 2, None)
+    monkeypatch.setenv("FHE_GPU_DEVICES", "1, 3")
+    assert fg.env_defaults() == ("negacyclic", 1, [1, 3])
+    assert fg.env_defaults("compat", 5, None) == ("compat", 5, None)
+    assert fg.env_defaults(None, None, [4]) == ("negacyclic", 4, [4])
+    monkeypatch.setenv("FHE_GPU_DEVICES", "a,b")
+    with pytest.raises(fg.FHEError):
+        fg.env_defaults()
+
+
+def test_env_defaults_js():
+    import shutil
+    import subprocess
+
+    if not shutil.which("node"):
+        pytest.skip("node not installed")
+    js = os.path.join(ROOT, "node-fhe-accelerate_amd", "lib", "engine.js")
+    code = (f"const e=require({js!r});const r=[];"
+            "process.env.FHE_GPU_DEVICES='0,1';r.push(e.envDefaults({}));"
+            "process.env.FHE_NTT_MODE='negacyclic';process.env.FHE_GPU_DEVICES='3';r.push(e.envDefaults({}));"
+            "r.push(e.envDefaults({mode:'compat',device:2}));"
+            "let bad=false;process.env.FHE_GPU_DEVICES='x';try{e.envDefaults({})}catch(_){bad=true}r.push(bad);"
+            "console.log(JSON.stringify(r));")
+    env = {k: v for k, v in os.environ.items() if k not in ("FHE_NTT_MODE", "FHE_GPU_DEVICES")}
+    out = subprocess.run(["node", "-e", code], capture_output=True, text=True, env=env, check=True).stdout
+    import json
+
+    r = json.loads(out)
+    assert r[0] == {"mode": "compat", "device": 0, "devices": [0, 1]}
+    assert r[1] == {"mode": "negacyclic", "device": 3}
+    assert r[2] == {"mode": "compat", "device": 2}
+    assert r[3] is True
