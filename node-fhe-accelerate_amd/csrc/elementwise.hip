@@ -251,6 +251,7 @@ __device__ __forceinline__ uint64_t mont_word(uint64_t a, uint64_t b, uint64_t q
         const uint32_t m = (uint32_t)p * (uint32_t)qinv;
         return (p + (uint64_t)m * q) >> 32;
     }
+    if (word == 65) return wmont(a, b, q, qinv);  // q >= 2^62: canonical
     return mont64(a, b, q, qinv);  // [0, 2q) for q < 2^62
 }
 __global__ void __launch_bounds__(kBlock)
@@ -265,6 +266,10 @@ k_mac_keys(const uint64_t *__restrict__ x, const uint64_t *__restrict__ g, uint6
             uint64_t acc = 0;
             for (uint32_t r = 0; r < rows; ++r) {
                 const uint64_t t = mont_word(x[(b * rows + r) * n + c], g[((size_t)r * k1 + kj) * n + c], m.q, m.qinv, word);
+                if (word == 65) {  // canonical terms; the sum may carry out of 64 bits
+                    acc = wadd(acc, t, m.q);
+                    continue;
+                }
                 acc += t;  // < 4q
                 acc = acc >= 2 * m.q ? acc - 2 * m.q : acc;
             }

@@ -347,6 +347,22 @@ __device__ __forceinline__ uint64_t mod64_slow(uint64_t x, uint64_t q, uint64_t 
     return r >= q ? r - q : r;
 }
 
+// Moduli up to 2^64 (ntt_wide.hip, the composed key MAC): a * b * 2^-64 mod q, canonical, for a, b < q and any odd q < 2^64:
+// (a b + m q) / 2^64 < 2q, and its 65th bit is the carry of the high sum.
+__device__ __forceinline__ uint64_t wmont(uint64_t a, uint64_t b, uint64_t q, uint64_t qinv) {
+    const uint64_t lo = a * b, hi = __umul64hi(a, b);
+    const uint64_t mh = __umul64hi(lo * qinv, q);
+    const uint64_t s = hi + mh;
+    const bool c1 = s < hi;
+    const uint64_t s2 = s + (lo != 0);  // low words: lo + lo(m q) == 0 mod 2^64, carry iff lo != 0
+    const bool c2 = s2 < s;
+    return (c1 || c2 || s2 >= q) ? s2 - q : s2;
+}
+__device__ __forceinline__ uint64_t wadd(uint64_t a, uint64_t b, uint64_t q) {
+    const uint64_t s = a + b;
+    return (s < a || s >= q) ? s - q : s;
+}
+__device__ __forceinline__ uint64_t wsub(uint64_t a, uint64_t b, uint64_t q) { return a >= b ? a - b : a - b + q; }
 // Load a u64 coefficient into the lazy range [0, lim) of word W.
 template <typename W>
 __device__ __forceinline__ W load_lazy(uint64_t x, uint64_t lim, uint64_t q, uint64_t mu) {

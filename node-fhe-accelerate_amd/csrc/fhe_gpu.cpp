@@ -85,6 +85,7 @@ FHE_NS::Tw<W> make_tw(u64 w, u64 q) {
 // ---------------------------------------------------------------- context
 struct Tables {
     void *twf = nullptr, *twi = nullptr;
+    void *wtf = nullptr, *wti = nullptr;  // q >= 2^62: Montgomery-form stage tables (ntt_wide.hip)
 };
 
 }  // namespace
@@ -93,6 +94,7 @@ struct fhe_ctx {
     u32 n = 0, logn = 0;
     u64 q = 0, psi = 0, psi_inv = 0, inv_n = 0;
     int mode = 0, device = 0, word = 64;
+    bool wide = false;  // q >= 2^62: transforms in ntt_wide.hip, fused ciphertext kernels unavailable
     hipStream_t own_stream = nullptr, stream = nullptr;
     Tables tab;
     FHE_NS::Plan plan{};
@@ -218,6 +220,37 @@ int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
     return FHE_OK;
 }
 
+// q >= 2^62 (ntt_wide.hip): the same stage-major twiddles in Montgomery form
+// (w 2^64 mod q) plus the Montgomery constants of WideArgs.
+int build_wide_tables(fhe_ctx *c) {
+    const u32 n = c->n, L = c->logn;
+    const u64 q = c->q;
+    const u64 R = (u64)((((u128)1) << 64) % q);
+    std::vector<u64> twf(n), twi(n);
+    twf[0] = twi[0] = R;
+    for (u32 s = 0; s < L; ++s)
+        for (u32 j = 0; j < (1u << s); ++j) {
+            const u64 ex = c->mode == FHE_MODE_COMPAT ? (u64)j * (n >> (s + 1)) : (u64)(2 * j + 1) * (n >> (s + 1));
+            twf[(1u << s) + j] = mulmod(c->fwd_tw[ex], R, q);
+            twi[(1u << s) + j] = mulmod(c->inv_tw[ex], R, q);
+        }
+    const size_t bytes = sizeof(u64) * n;
+    HIP_TRY(hipMalloc(&c->tab.wtf, bytes), "hipMalloc(twiddles)");
+    HIP_TRY(hipMalloc(&c->tab.wti, bytes), "hipMalloc(twiddles)");
+    HIP_TRY(hipMemcpy(c->tab.wtf, twf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(twiddles)");
+    HIP_TRY(hipMemcpy(c->tab.wti, twi.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(twiddles)");
+    FHE_NS::WideArgs &W = c->plan.wa;
+    W.twf = (const u64 *)c->tab.wtf;
+    W.twi = (const u64 *)c->tab.wti;
+    W.q = q;
+    W.qinv = neg_inv_pow2<u64>(q);
+    W.mu = (u64)((((u128)1) << 64) / q);
+    W.r2 = mulmod(R, R, q);
+    W.ninv_m = mulmod(c->inv_n, R, q);
+    W.ninv_r2 = mulmod(W.ninv_m, R, q);
+    return FHE_OK;
+}
+
 void free_pipe(fhe_ctx *c) {
     auto &P = c->pipe;
     for (int i = 0; i < fhe_ctx::Pipe::kSlots; ++i) {
@@ -236,7 +269,7 @@ void free_pipe(fhe_ctx *c) {
 }
 
 void free_tables(fhe_ctx *c) {
-    void *p[2] = {c->tab.twf, c->tab.twi};
+    void *p[4] = {c->tab.twf, c->tab.twi, c->tab.wtf, c->tab.wti};
     for (void *x : p)
         if (x) (void)hipFree(x);
     c->tab = Tables{};
@@ -257,7 +290,7 @@ FHE_NS::ModConsts mod_consts(u64 q) {
     m.q = q;
     m.mu = q > 1 ? (u64)((((u128)1) << 64) / q) : 0;
     m.fast = (q & 1) && q > 1 && !(q >> 63);
-    if (m.fast) {
+    if ((q & 1) && q > 1) {  // Montgomery constants for any odd q (the key MAC at q >= 2^62 uses them)
         m.qinv = neg_inv_pow2<u64>(q);
         const u64 R = (u64)((((u128)1) << 64) % q);
         m.r2 = mulmod(R, R, q);
@@ -551,6 +584,7 @@ static int check_common(const fhe_ctx *c, int where, size_t batch) {
 static int check_fused(const fhe_ctx *c, const char *what) {
     if ((int)c->logn > FHE_NS::kMaxFusedLogN)
         return fail(FHE_ERR_UNSUPPORTED, std::string(what) + " implemented for degrees up to 16384");
+    if (c->wide) return fail(FHE_ERR_UNSUPPORTED, std::string(what) + " implemented for moduli below 2^62");
     return FHE_OK;
 }
 static int check_relin_decomp(uint32_t base_log, uint32_t level) {
@@ -558,6 +592,10 @@ static int check_relin_decomp(uint32_t base_log, uint32_t level) {
         return fail(FHE_ERR_INVALID_ARG, "invalid decomposition (base_log, level)");
     return FHE_OK;
 }
+
+// Montgomery word of the prepared keys for launch_mac_keys: 32 / 64, or 65
+// for q >= 2^62 (canonical Montgomery products with the carry bit).
+static int mac_word(const fhe_ctx *c) { return c->wide ? 65 : c->word; }
 
 // Composed (unfused) ciphertext multiply for n > 16384: 4 forward
 // transforms, tensor, 3 inverse transforms through a temporary.
@@ -583,7 +621,7 @@ static int ct_mul_device(fhe_ctx *c, const u64 *x, const u64 *y, u64 *out, size_
         HIP_TRY(FHE_NS::launch_tensor_ntt(mod_consts(c->q), x, y, out, c->n, batch, c->stream), "tensor kernel");
         return FHE_OK;
     }
-    if ((int)c->logn > FHE_NS::kMaxFusedLogN) return ct_mul_composed(c, x, y, out, batch);
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN || c->wide) return ct_mul_composed(c, x, y, out, batch);
     HIP_TRY(FHE_NS::launch_ct_mul(c->plan, x, y, out, batch), "ct_mul kernel");
     return FHE_OK;
 }
@@ -616,7 +654,7 @@ static int extprod_composed(fhe_ctx *c, uint32_t k1, uint32_t level, uint32_t ba
         hipError_t e = FHE_NS::launch_decompose(m, g, dig, (u32)n, nb * k1, base_log, level, c->stream);
         if (e == hipSuccess) e = FHE_NS::launch_fwd(c->plan, dig, dig, nb * rows, 0);
         if (e == hipSuccess)
-            e = FHE_NS::launch_mac_keys(m, c->word, dig, ggsw, o, (u32)n, nb, (u32)rows, k1, 0, c->stream);
+            e = FHE_NS::launch_mac_keys(m, mac_word(c), dig, ggsw, o, (u32)n, nb, (u32)rows, k1, 0, c->stream);
         if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, o, o, nb * k1);
         if (e != hipSuccess) return hip_fail(e, "composed external product");
     }
@@ -640,7 +678,7 @@ static int relin_composed(fhe_ctx *c, uint32_t base_log, uint32_t level, const u
         u64 *o = out + b0 * 2 * n;
         hipError_t e = FHE_NS::launch_relin_digits(x, dig, (u32)n, nb, base_log, level, c->stream);
         if (e == hipSuccess) e = FHE_NS::launch_fwd(c->plan, dig, dig, nb * level, 0);
-        if (e == hipSuccess) e = FHE_NS::launch_mac_keys(m, c->word, dig, rlk, o, (u32)n, nb, level, 2, 1, c->stream);
+        if (e == hipSuccess) e = FHE_NS::launch_mac_keys(m, mac_word(c), dig, rlk, o, (u32)n, nb, level, 2, 1, c->stream);
         if (e == hipSuccess) e = FHE_NS::launch_inv(c->plan, o, o, nb * 2);
         if (e == hipSuccess) e = FHE_NS::launch_add_rows(m, o, x, (u32)n, nb, 2, 3, c->stream);
         if (e != hipSuccess) return hip_fail(e, "composed relinearisation");
@@ -658,7 +696,7 @@ static int relin_device(fhe_ctx *c, uint32_t base_log, uint32_t level, const u64
                 "hipMemcpy2D");
         return FHE_OK;
     }
-    if ((int)c->logn > FHE_NS::kMaxFusedLogN) return relin_composed(c, base_log, level, ct3, rlk, out, batch);
+    if ((int)c->logn > FHE_NS::kMaxFusedLogN || c->wide) return relin_composed(c, base_log, level, ct3, rlk, out, batch);
     HIP_TRY(FHE_NS::launch_relin(c->plan, (int)level, (int)base_log, ct3, rlk, out, batch), "relin kernel");
     return FHE_OK;
 }
@@ -706,7 +744,6 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     while ((1u << logn) < n) ++logn;
     if ((int)logn > FHE_NS::kMaxLogN)
         return fail(FHE_ERR_UNSUPPORTED, "GPU kernels implement degrees up to 16384 (got " + std::to_string(n) + ")");
-    if (q >> 62) return fail(FHE_ERR_UNSUPPORTED, "GPU kernels implement moduli below 2^62");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
         return fail(FHE_ERR_DEVICE, "no HIP device available (the backend has no CPU fallback)");
@@ -715,6 +752,7 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     fhe_ctx *c = new fhe_ctx();
     c->n = n; c->logn = logn; c->q = q; c->psi = psi; c->mode = mode; c->device = device;
     c->word = q < (1ull << 30) ? 32 : 64;
+    c->wide = (q >> 62) != 0;
     if (!invmod(psi, q, c->psi_inv) || !invmod(n, q, c->inv_n)) {
         delete c;
         return fail(FHE_ERR_NO_ROOT, "Could not find primitive root for given parameters");
@@ -728,6 +766,7 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     }
     DeviceGuard g(device);
     int rc = c->word == 32 ? build_tables<u32>(c, c->plan.a32) : build_tables<u64>(c, c->plan.a64);
+    if (rc == FHE_OK && c->wide) rc = build_wide_tables(c);
     if (rc == FHE_OK && (int)logn > FHE_NS::kMaxFusedLogN) {
         // two-pass transforms (ntt_big.hip): 2 x 256 MiB of chunk scratch
         c->plan.big_chunk = ((size_t)1 << 25) >> logn;
@@ -759,6 +798,7 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     c->stream = c->own_stream;
     c->plan.logn = logn;
     c->plan.word = c->word;
+    c->plan.wide = c->wide;
     c->plan.lazy = c->word == 32 && (u128)(4 + 2 * logn) * q <= ((u128)1 << 32);
     c->plan.stream = c->stream;
     c->plan.big_sync = &c->big_sync;
@@ -947,7 +987,9 @@ int fhe_poly_mul_scalar_batch(fhe_ctx *c, const uint64_t *a, uint64_t scalar, ui
 // GLWE dimension: the fused kernels take k = 1 (and N <= 16384); other
 // shapes run composed (extprod_composed).
 constexpr uint32_t kMaxGlweDim = 16;
-static bool fused_tfhe(const fhe_ctx *c, uint32_t k) { return k == 1 && (int)c->logn <= FHE_NS::kMaxFusedLogN; }
+static bool fused_tfhe(const fhe_ctx *c, uint32_t k) {
+    return k == 1 && (int)c->logn <= FHE_NS::kMaxFusedLogN && !c->wide;
+}
 static int check_decomp(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level) {
     (void)c;
     if (k == 0 || k > kMaxGlweDim) return fail(FHE_ERR_UNSUPPORTED, "GLWE dimension k must be between 1 and 16");

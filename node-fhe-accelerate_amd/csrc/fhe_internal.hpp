@@ -22,9 +22,20 @@ struct BigSync {
     hipStream_t last = nullptr;
 };
 
+// Moduli 2^62 <= q < 2^64 (ntt_wide.hip): canonical arithmetic, twiddles in
+// Montgomery form (w 2^64 mod q), stage-major like NttArgs' tables.
+struct WideArgs {
+    const uint64_t *twf, *twi;
+    uint64_t q, qinv, mu;   // qinv = -q^-1 mod 2^64, mu = floor(2^64 / q)
+    uint64_t r2;            // 2^128 mod q
+    uint64_t ninv_m;        // N^-1 2^64 mod q
+    uint64_t ninv_r2;       // N^-1 2^128 mod q (after a Montgomery pointwise product)
+};
+
 struct Plan {
     uint32_t logn;
     int word;   // 32 or 64
+    int wide;   // q >= 2^62: every transform takes ntt_wide.hip
     int lazy;   // 32-bit path with (4 + 2L) q <= 2^32: forward stages skip reductions
     hipStream_t stream;
     // N > 2^kMaxFusedLogN (ntt_big.hip): two chunk-sized scratch buffers
@@ -33,6 +44,7 @@ struct Plan {
     BigSync *big_sync; // owned by the context
     NttArgs<uint32_t> a32;
     NttArgs<uint64_t> a64;
+    WideArgs wa;  // wide != 0
 };
 
 constexpr int kMinLogN = 2;
@@ -47,6 +59,8 @@ hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t b
 hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch);
 // c = inv(fwd(a) (.) fwd(b))  (PolynomialRing::multiply)
 hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
+// q >= 2^62 (Plan::wide), any N: op as launch_big
+hipError_t launch_wide(const Plan &p, int op, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
 // N > 2^kMaxFusedLogN: op 0 fwd, 1 fwd*R, 2 fwd (.) b, 3 inv, 4 polymul
 hipError_t launch_big(const Plan &p, int op, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
 // TFHE external product, GGSW already in NTT-Montgomery form.

@@ -170,10 +170,12 @@ static hipError_t fwd_any(const Plan &p, const uint64_t *in, uint64_t *out, size
 }
 
 hipError_t launch_fwd(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch, int epi) {
+    if (p.wide) return launch_wide(p, epi == 1 ? 1 : 0, in, nullptr, out, batch);
     if (p.logn > kMaxFusedLogN) return launch_big(p, epi == 1 ? 1 : 0, in, nullptr, out, batch);
     return fwd_any(p, in, out, batch, epi, nullptr);
 }
 hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch) {
+    if (p.wide) return launch_wide(p, 2, a, w, out, batch);
     if (p.logn > kMaxFusedLogN) return launch_big(p, 2, a, w, out, batch);
     return fwd_any(p, a, out, batch, 0, w);
 }

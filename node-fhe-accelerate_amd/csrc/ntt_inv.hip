@@ -268,14 +268,16 @@ static hipError_t inv_any(const Plan &p, const uint64_t *a, const uint64_t *b, u
 }
 
 hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch) {
+    if (p.wide) return launch_wide(p, 3, in, nullptr, out, batch);
     if (p.logn > kMaxFusedLogN) return launch_big(p, 3, in, nullptr, out, batch);
     return inv_any(p, in, nullptr, out, batch);
 }
 hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch) {
     // The HBM stash writes fwd(a) into c before b is read: if c aliases b,
     // transform b first (the pointwise product commutes).
-    if (p.logn > kMaxFusedLogN) return launch_big(p, 4, a, b, c, batch);
+    if (p.logn > kMaxFusedLogN && !p.wide) return launch_big(p, 4, a, b, c, batch);
     if (c == b) { const uint64_t *t = a; a = b; b = t; }
+    if (p.wide) return launch_wide(p, 4, a, b, c, batch);
     return inv_any(p, a, b, c, batch);
 }
 

@@ -59,7 +59,6 @@ def test_version_and_detect():
         (131072, 97, -2, "Polynomial degree must be between 4 and 65536"),
         (8, 96, -3, "Modulus must be odd"),
         (16, 17, -4, "Modulus is not NTT-friendly"),
-        (8, 4611686018428108801, -10, "moduli below 2^62"),  # q > 2^62, NTT-friendly
     ],
 )
 def test_ctx_validation_messages(n, q, code, msg):
@@ -67,13 +66,6 @@ def test_ctx_validation_messages(n, q, code, msg):
         fhe_gpu.NTTProcessor(n, q)
     assert ei.value.code == code
     assert msg in str(ei.value)
-
-
-def test_wide_modulus_unsupported():
-    q = 4611686018428108801  # > 2^62, prime, 1 mod 2^16
-    with pytest.raises(FHEError) as ei:
-        fhe_gpu.NTTProcessor(1024, q)
-    assert ei.value.code == -10
 
 
 def test_no_cpu_fallback_without_device(gpu_available):

@@ -1,0 +1,132 @@
+"""Moduli 2^62 <= q < 2^64 (ntt_wide.hip): the reference takes any odd u64 q
+whose root search succeeds (ntt_processor.cpp:140-153; every product is a
+128-bit %), so the GPU path must too.  HIP vs the CPU oracle, bit-exact;
+ring ops, the composed ciphertext paths, and the fused-only entry points'
+FHE_ERR_UNSUPPORTED."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+Q62 = 4611686018429485057     # 2^62 + 2^21 + 1 (smallest prime above 2^62 that is 1 mod 2^17)
+Q63 = 9223370937344327681     # just below 2^63
+QG = 18446744069414584321     # 2^64 - 2^32 + 1 (above 2^63: sums carry out of 64 bits)
+WIDE = [Q62, Q63, QG]
+
+
+@pytest.fixture(scope="module")
+def fg():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import fhe_gpu
+
+    return fhe_gpu
+
+
+@pytest.mark.parametrize("n", [4, 8, 64, 1024, 4096, 16384, 32768, 65536])
+@pytest.mark.parametrize("q", WIDE)
+def test_wide_transforms_vs_oracle(fg, n, q):
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    assert r.primitive_root == t.psi
+    b = 2 if n > 16384 else 3 if n >= 4096 else 9
+    x = oracle.splitmix_fill(n * 7 + 1, q, b * n).reshape(b, n)
+    y = oracle.splitmix_fill(n * 7 + 2, q, b * n).reshape(b, n)
+    assert (r.forward_ntt(x) == t.forward(x)).all()
+    assert (r.inverse_ntt(x) == t.inverse(x)).all()
+    assert (r.multiply(x, y) == t.polymul(x, y)).all()
+    assert (r.forward_ntt_mul(x, y) == t.fwd_mul(x, y)).all()
+    assert (r.pointwise_multiply(x, y) == oracle.pointwise(q, x.ravel(), y.ravel()).reshape(b, n)).all()
+    assert (r.add(x, y) == oracle.poly_add(q, x.ravel(), y.ravel()).reshape(b, n)).all()
+    assert (r.subtract(x, y) == oracle.poly_sub(q, x.ravel(), y.ravel()).reshape(b, n)).all()
+
+
+@pytest.mark.parametrize("n,q", [(1024, QG), (16384, Q63), (32768, QG)])
+def test_wide_raw_u64_inputs(fg, n, q):
+    """Any u64 word behaves as x mod q (values >= q, the top of the range)."""
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    rng = np.random.default_rng(n)
+    x = rng.integers(0, 2 ** 64 - 1, (2, n), dtype=np.uint64, endpoint=True)
+    x[0, :3] = [0, q, 2 ** 64 - 1]
+    y = rng.integers(0, 2 ** 64 - 1, (2, n), dtype=np.uint64, endpoint=True)
+    assert (r.forward_ntt(x) == t.forward(x)).all()
+    assert (r.inverse_ntt(x) == t.inverse(x)).all()
+    assert (r.multiply(x, y) == t.polymul(x, y)).all()
+    assert (r.forward_ntt_mul(x, y) == t.fwd_mul(x, y)).all()
+
+
+@pytest.mark.parametrize("q", WIDE)
+def test_wide_in_place_and_aliasing(fg, q):
+    import torch
+
+    n = 2048
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    x = oracle.splitmix_fill(11, q, 4 * n).reshape(4, n)
+    y = oracle.splitmix_fill(12, q, 4 * n).reshape(4, n)
+    dx = torch.from_numpy(x.view(np.int64)).cuda()
+    dy = torch.from_numpy(y.view(np.int64)).cuda()
+    r.multiply(dx, dy, out=dy)  # out aliases b
+    torch.cuda.synchronize()
+    assert (dy.cpu().numpy().view(np.uint64) == t.polymul(x, y)).all()
+    r.forward_ntt(dx, out=dx)  # in place
+    torch.cuda.synchronize()
+    assert (dx.cpu().numpy().view(np.uint64) == t.forward(x)).all()
+
+
+@pytest.mark.parametrize("q", [Q62, QG])
+def test_wide_negacyclic_ring_product(fg, q):
+    n = 4096
+    r = fg.PolynomialRing(n, q, mode="negacyclic")
+    x = oracle.splitmix_fill(5, q, n).reshape(1, n)
+    X = np.zeros((1, n), np.uint64)
+    X[0, 1] = 1
+    expect = np.roll(x, 1, axis=1)
+    expect[0, 0] = (q - int(x[0, -1])) % q
+    assert (r.multiply(x, X) == expect).all()
+    assert (r.inverse_ntt(r.forward_ntt(x)) == x).all()
+
+
+@pytest.mark.parametrize("n,q", [(1024, QG), (4096, Q62)])
+def test_wide_ciphertext_multiply_and_relinearize(fg, n, q):
+    """Composed paths (transforms + the exact pointwise tensor + the canonical
+    Montgomery key MAC) at q >= 2^62, vs the oracle's reference loops."""
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    eng = fg.EncryptionEngine(r)
+    x = oracle.splitmix_fill(21, q, 2 * 2 * n).reshape(2, 2, n)
+    y = oracle.splitmix_fill(22, q, 2 * 2 * n).reshape(2, 2, n)
+    ct3 = eng.multiply(x, y)
+    for i in range(2):
+        assert (ct3[i] == t.ct_multiply(x[i], y[i])).all(), i
+    bl, lv = 16, 4
+    rlk = oracle.splitmix_fill(23, q, lv * 2 * n).reshape(lv, 2, n)
+    out = eng.relinearize(ct3, fg.EvaluationKey(r, rlk, bl))
+    for i in range(2):
+        assert (out[i] == t.relinearize(bl, lv, ct3[i], rlk)).all(), i
+
+
+@pytest.mark.parametrize("q", [Q62, QG])
+def test_wide_external_product(fg, q):
+    n, k, bl, lv = 1024, 1, 20, 2
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    ggsw = oracle.splitmix_fill(31, q, (k + 1) * lv * (k + 1) * n).reshape((k + 1) * lv, k + 1, n)
+    glwe = oracle.splitmix_fill(32, q, 3 * (k + 1) * n).reshape(3, k + 1, n)
+    got = fg.ExternalProduct(r, ggsw, bl, lv, k)(glwe)
+    for i in range(3):
+        assert (got[i] == t.external_product(k, bl, lv, glwe[i], ggsw)).all(), i
+
+
+def test_wide_fused_only_entry_points_report_unsupported(fg):
+    """encrypt / decrypt / add_plain run only as fused kernels (lazy
+    arithmetic): at q >= 2^62 their preparation reports FHE_ERR_UNSUPPORTED."""
+    r = fg.PolynomialRing(1024, QG)
+    with pytest.raises(fg.FHEError) as ei:
+        fg.PublicKey(r, np.zeros((2, 1024), np.uint64))
+    assert ei.value.code == -10 and "2^62" in str(ei.value)
