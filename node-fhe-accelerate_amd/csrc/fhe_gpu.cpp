@@ -67,6 +67,31 @@ bool invmod(u64 a, u64 q, u64 &out) {
     out = (u64)t;
     return true;
 }
+// NTTProcessor::mod_inverse (ntt_processor.cpp:63-89) as the reference
+// computes it: a signed extended Euclid on int64 casts of a % m and m, so
+// for m >= 2^63 (negative as int64) the loop stops at once and the result is
+// not an inverse (1 for a >= 2^63, else 0).  The compat transform uses these
+// values for psi^-1 and N^-1 (:179-182), so its inverse matches the
+// reference bit for bit at every q -- at q >= 2^63 that is the reference's
+// all-zero inverse.  Wrapping arithmetic; x / 0 = 0 and x % 0 = x (the
+// AArch64 semantics of the platform the reference targets).
+u64 ref_mod_inverse(u64 a, u64 m) {
+    if (m <= 1) return 0;
+    const int64_t m0 = (int64_t)m;
+    int64_t x0 = 0, x1 = 1, as = (int64_t)(a % m), ms = (int64_t)m;
+    while (as > 1) {
+        const int64_t qt = ms == 0 ? 0 : (ms == -1 ? -as : as / ms);
+        int64_t t = ms;
+        ms = ms == 0 ? as : (ms == -1 ? 0 : as % ms);
+        as = t;
+        t = x0;
+        x0 = (int64_t)((u64)x1 - (u64)qt * (u64)x0);
+        x1 = t;
+    }
+    if (x1 < 0) x1 = (int64_t)((u64)x1 + (u64)m0);
+    return (u64)x1;
+}
+
 template <typename W>
 W neg_inv_pow2(W q) {  // -q^-1 mod 2^W (q odd), Newton
     W x = q;
@@ -756,6 +781,10 @@ int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out) 
     if (!invmod(psi, q, c->psi_inv) || !invmod(n, q, c->inv_n)) {
         delete c;
         return fail(FHE_ERR_NO_ROOT, "Could not find primitive root for given parameters");
+    }
+    if (mode == FHE_MODE_COMPAT) {  // the reference's own constants (equal to the true inverses below 2^63)
+        c->psi_inv = ref_mod_inverse(psi, q);
+        c->inv_n = ref_mod_inverse(n, q);
     }
     c->fwd_tw.resize(n);
     c->inv_tw.resize(n);

@@ -2,7 +2,14 @@
 whose root search succeeds (ntt_processor.cpp:140-153; every product is a
 128-bit %), so the GPU path must too.  HIP vs the CPU oracle, bit-exact;
 ring ops, the composed ciphertext paths, and the fused-only entry points'
-FHE_ERR_UNSUPPORTED."""
+FHE_ERR_UNSUPPORTED.
+
+At q >= 2^63 the reference's NTTProcessor::mod_inverse (ntt_processor.cpp:
+63-89) runs its signed Euclid on a negative int64 modulus and returns 0 for
+N^-1 (1 for psi^-1), so its inverse transform -- and everything built on it
+-- yields zeros; the compat mode reproduces that (the oracle restates the
+same loop), while negacyclic mode, which the reference lacks, uses the true
+inverses and is checked as a ring product."""
 import numpy as np
 import pytest
 
