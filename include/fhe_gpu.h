@@ -81,7 +81,11 @@ int fhe_detect(fhe_hw_caps *caps);
  * (ntt_processor.cpp:134-208, polynomial_ring.cpp:213-222).
  * Validation order and messages follow the reference constructor.  n must
  * be a power of two in [4, 65536]; the GPU kernels implement every such n
- * and q < 2^62 (FHE_ERR_UNSUPPORTED otherwise).  n > 16384 runs as a
+ * and every odd q whose root search succeeds: q < 2^62 in the lazy kernel
+ * family, 2^62 <= q < 2^64 in the canonical one (ntt_wide.hip; there the
+ * fused-only encrypt / decrypt / add_plain return FHE_ERR_UNSUPPORTED and
+ * compat mode keeps the reference's psi^-1 and N^-1, which are not inverses
+ * at q >= 2^63, ntt_processor.cpp:63-89).  n > 16384 runs as a
  * two-pass row/column split and the context holds 512 MiB of device
  * scratch (every entry point takes such contexts: fused kernels up to
  * n = 16384, composed ones above).
@@ -122,7 +126,7 @@ typedef struct {
     uint64_t psi_inv;
     uint64_t inv_n;        /* N^-1 mod q */
     int32_t mode;
-    int32_t word_bits;     /* 32 (q < 2^30) or 64 (q < 2^62) kernel arithmetic */
+    int32_t word_bits;     /* 32 (q < 2^30) or 64 (q < 2^64) kernel arithmetic */
     int32_t device;
     int32_t polys_per_block;
     int32_t threads_per_block;

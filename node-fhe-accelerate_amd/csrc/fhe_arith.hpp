@@ -137,6 +137,10 @@ __device__ __forceinline__ uint64_t sub_add64(uint64_t a, uint64_t b, uint64_t c
 
 // Twiddle with its Shoup companion w' = floor(w * 2^W / q).
 template <typename W> struct Tw { W w, wp; };
+// Two Shoup multipliers of a stage-0 butterfly that folds a scaling into
+// the stage (Arith::ct_rscale, Arith::gs_scaled): .a for the first
+// operand / output, .b for the second (ntt_core.hpp NttArgs).
+template <typename W> struct Scale { Tw<W> a, b; };
 
 // 32-bit forward (CT) twiddle tables hold -w mod 2^32 in Tw::w (Arith::ct).
 #ifndef FHE_NEG_FWD_TW
@@ -317,9 +321,9 @@ struct Arith {
     // Stage-0 butterfly that also multiplies by R = 2^W (twiddle 1 -> R):
     // puts the transform in Montgomery form for a following pointwise
     // Montgomery product.  Outputs in [0, 4q) for any inputs < 2^W.
-    __device__ __forceinline__ void ct_rscale(W &x, W &y, Tw<W> r) const {
-        W a = shoup(x, r);
-        W b = shoup(y, r);
+    __device__ __forceinline__ void ct_rscale(W &x, W &y, Scale<W> r) const {
+        W a = shoup(x, r.a);
+        W b = shoup(y, r.b);
         x = a + b;
         y = sub2q(a, b);
     }
@@ -331,11 +335,11 @@ struct Arith {
         y = shoup_inv(d, t);
     }
     // Last GS stage with the N^-1 scaling folded in (w = 1 at stage 0).
-    __device__ __forceinline__ void gs_scaled(W &x, W &y, Tw<W> ninv) const {
+    __device__ __forceinline__ void gs_scaled(W &x, W &y, Scale<W> ninv) const {
         W s = x + y;
         W d = sub2q(x, y);
-        x = shoup_inv(s, ninv);
-        y = shoup_inv(d, ninv);
+        x = shoup_inv(s, ninv.a);
+        y = shoup_inv(d, ninv.b);
     }
 };
 

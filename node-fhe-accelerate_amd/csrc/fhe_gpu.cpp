@@ -238,8 +238,13 @@ int build_tables(fhe_ctx *c, FHE_NS::NttArgs<W> &A) {
     A.ar.r2 = (W)mulmod(R, R, q);
     A.q64 = q;
     A.mu64 = (u64)((((u128)1) << 64) / q);
-    A.ninv = make_tw<W>(c->inv_n, q);
-    A.ninv_r = make_tw<W>(ninv_r, q);
+    // stage-0 twiddle w0 (1 in compat mode, psi^(N/2) in negacyclic mode)
+    // and its inverse, folded into the scaled stage-0 butterflies
+    const u64 w0 = L ? c->fwd_tw[c->mode == FHE_MODE_COMPAT ? 0 : n / 2] : 1;
+    const u64 w0i = L ? c->inv_tw[c->mode == FHE_MODE_COMPAT ? 0 : n / 2] : 1;
+    A.ninv = {make_tw<W>(c->inv_n, q), make_tw<W>(mulmod(c->inv_n, w0i, q), q)};
+    A.ninv_r = {make_tw<W>(ninv_r, q), make_tw<W>(mulmod(ninv_r, w0i, q), q)};
+    A.rs = {make_tw<W>(R, q), make_tw<W>(mulmod(R, w0, q), q)};
     A.rmod = make_tw<W>(R, q);
     A.one = make_tw<W>(1, q);
     return FHE_OK;
@@ -1607,19 +1612,31 @@ static int check_br(const fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t le
 // ExtProd(bsk_i, d) composed (decompose, batched transforms, key MAC,
 // inverse), cur + product -- ping-ponging two device buffers; skipped steps
 // (r == 0) copy cur through.  Every temporary (one digit buffer for all
-// steps) is allocated once, stream-ordered; nothing synchronises the host.
+// steps) is allocated once, stream-ordered -- or carved from `scratch` (the
+// context's persistent buffer of blind_rotate_scratch_bytes, when the call
+// is captured into a hipGraph); nothing synchronises the host.
+static size_t blind_rotate_scratch_bytes(const fhe_ctx *c, uint32_t k, uint32_t level, size_t batch) {
+    return 3 * batch * (k + 1) * c->n * 8 + extprod_digit_words(c, k + 1, level, batch) * 8;
+}
 static int blind_rotate_composed(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t level, uint32_t lwe_dim,
                                  const u64 *lwe_a, const u64 *lwe_b, uint64_t lwe_q, const u64 *bsk_ntt, u64 *acc,
-                                 size_t batch) {
+                                 size_t batch, u64 *scratch = nullptr) {
     const size_t n = c->n, k1 = k + 1, bytes = batch * k1 * n * 8;
     const size_t ggsw_words = k1 * level * k1 * n;
     const FHE_NS::ModConsts m = mod_consts(c->q);
     StreamTemp tmp(c->stream);
     u64 *cur = nullptr, *d = nullptr, *ep = nullptr, *dig = nullptr;
-    FHE_TRY(tmp.alloc(bytes, cur));
-    FHE_TRY(tmp.alloc(bytes, d));
-    FHE_TRY(tmp.alloc(bytes, ep));
-    FHE_TRY(tmp.alloc(extprod_digit_words(c, (uint32_t)k1, level, batch) * 8, dig));
+    if (scratch) {
+        cur = scratch;
+        d = cur + bytes / 8;
+        ep = d + bytes / 8;
+        dig = ep + bytes / 8;
+    } else {
+        FHE_TRY(tmp.alloc(bytes, cur));
+        FHE_TRY(tmp.alloc(bytes, d));
+        FHE_TRY(tmp.alloc(bytes, ep));
+        FHE_TRY(tmp.alloc(extprod_digit_words(c, (uint32_t)k1, level, batch) * 8, dig));
+    }
     HIP_TRY(FHE_NS::launch_rotate(m, acc, cur, (uint32_t)n, (uint32_t)k1, batch, nullptr, lwe_b, lwe_q, c->stream),
             "rotate kernel");
     for (uint32_t i = 0; i < lwe_dim; ++i) {
@@ -1709,7 +1726,14 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     FHE_TRY(hs.map(where, lwe_b, batch * 8, 1));
     FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
     FHE_TRY(hs.map(where, acc, bytes, 3));
-    if (!fused_tfhe(c, k)) {
+    static const bool no_graph = std::getenv("FHE_NO_GRAPH") && std::getenv("FHE_NO_GRAPH")[0] == '1';
+    const bool composed = !fused_tfhe(c, k);
+    // composed steps (k > 1, N > 16384, q >= 2^62): six launches per CMux;
+    // device-resident calls with fused transforms are captured into the
+    // context's hipGraph below (persistent scratch, no stream allocations)
+    const bool composed_graph = composed && !no_graph && where == FHE_DEVICE && c->stream != nullptr && lwe_dim > 0 &&
+                                (int)c->logn <= FHE_NS::kMaxFusedLogN;
+    if (composed && !composed_graph) {
         FHE_TRY(blind_rotate_composed(c, k, base_log, level, lwe_dim, lwe_a, lwe_b, lwe_q, bsk_ntt, acc, batch));
         return where == FHE_HOST ? hs.finish() : FHE_OK;
     }
@@ -1717,21 +1741,22 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     // (ntt_br.hip); FHE_BR_PERSIST_MAX caps the batch it takes (0 = never).
     const char *pm = std::getenv("FHE_BR_PERSIST_MAX");
     const size_t persist_max = pm ? (size_t)std::strtoull(pm, nullptr, 10) : kBrPersistMax;
-    if (lwe_dim > 0 && batch <= persist_max && FHE_NS::br_persist_supported(c->plan, (int)k + 1)) {
+    if (!composed && lwe_dim > 0 && batch <= persist_max && FHE_NS::br_persist_supported(c->plan, (int)k + 1)) {
         HIP_TRY(FHE_NS::launch_br_persist(c->plan, (int)k + 1, (int)level, (int)base_log, acc, bsk_ntt, lwe_a, lwe_b,
                                           lwe_dim, lwe_q, batch),
                 "blind rotate kernel");
         return where == FHE_HOST ? hs.finish() : FHE_OK;
     }
     std::lock_guard<std::mutex> lk(c->br_mu);
-    if (c->br_tmp_bytes < bytes) {
+    const size_t need = composed ? blind_rotate_scratch_bytes(c, k, level, batch) : bytes;
+    if (c->br_tmp_bytes < need) {
         if (c->br.exec) { (void)hipGraphExecDestroy(c->br.exec); c->br.exec = nullptr; }
         if (c->br.graph) { (void)hipGraphDestroy(c->br.graph); c->br.graph = nullptr; }
         if (c->br_tmp) (void)hipFree(c->br_tmp);
         c->br_tmp = nullptr;
         c->br_tmp_bytes = 0;
-        HIP_TRY(hipMalloc(&c->br_tmp, bytes), "hipMalloc(blind rotate)");
-        c->br_tmp_bytes = bytes;
+        HIP_TRY(hipMalloc(&c->br_tmp, need), "hipMalloc(blind rotate)");
+        c->br_tmp_bytes = need;
     }
     u64 *tmp = (u64 *)c->br_tmp;
     // br_tmp may still be in use by a call enqueued on another stream
@@ -1741,6 +1766,9 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     // ping-ponging tmp <-> acc; the result is copied back into acc if it
     // ended in tmp.
     auto enqueue = [&]() -> hipError_t {
+        if (composed)
+            return blind_rotate_composed(c, k, base_log, level, lwe_dim, lwe_a, lwe_b, lwe_q, bsk_ntt, acc, batch, tmp)
+                           == FHE_OK ? hipSuccess : hipErrorLaunchFailure;
         hipError_t e = FHE_NS::launch_rotate(mod_consts(c->q), acc, tmp, c->n, k + 1, batch, nullptr, lwe_b, lwe_q,
                                              c->stream);
         u64 *cur = tmp, *nxt = acc;
@@ -1756,7 +1784,6 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     // a hipGraph and replayed while (buffers, shape, stream) are unchanged.
     // The legacy null stream cannot be captured; FHE_NO_GRAPH=1 disables
     // graphs.
-    static const bool no_graph = std::getenv("FHE_NO_GRAPH") && std::getenv("FHE_NO_GRAPH")[0] == '1';
     fhe_ctx::BrGraph &G = c->br;
     const bool same = G.exec && G.acc == acc && G.lwe_a == lwe_a && G.lwe_b == lwe_b && G.bsk == bsk_ntt &&
                       G.batch == batch && G.k == k && G.base_log == base_log && G.level == level &&

@@ -338,7 +338,7 @@ __device__ __forceinline__ void load_tw(uint32_t tau, const Tw<W> *__restrict__ 
 // RS (pass 0 only): global stage 0 multiplies by R (ct_rscale).
 template <int LOGN, int PASS, bool LAZY, typename W, bool RS = false>
 __device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                         const Arith<W> &ar, Tw<W> rmod = Tw<W>{}) {
+                                         const Arith<W> &ar, Scale<W> rmod = Scale<W>{}) {
     using P = PassTw<LOGN, PASS>;
     constexpr int R = P::R, NU = P::NU;
 #pragma unroll
@@ -360,7 +360,7 @@ __device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[
 // FOLD, global stage 0 (w = 1) applies the N^-1 (or N^-1 * R) scaling.
 template <int LOGN, int PASS, bool FOLD, typename W>
 __device__ __forceinline__ void inv_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                         const Arith<W> &ar, Tw<W> scale) {
+                                         const Arith<W> &ar, Scale<W> scale) {
     using P = PassTw<LOGN, PASS>;
     constexpr int S = P::S, R = P::R, NU = P::NU;
 #pragma unroll
@@ -399,7 +399,7 @@ __device__ __forceinline__ void fwd_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)
 }
 template <int LOGN, int PASS, int K, bool FOLD, typename W>
 __device__ __forceinline__ void inv_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                          const Arith<W> &ar, Tw<W> scale) {
+                                          const Arith<W> &ar, Scale<W> scale) {
     using P = PassTw<LOGN, PASS>;
     constexpr int S = P::S, R = P::R, NU = P::NU;
 #pragma unroll
@@ -431,7 +431,7 @@ __device__ __forceinline__ void fwd_stages(uint32_t tau, W (&v)[Geo<LOGN>::E], T
 }
 template <int LOGN, int PASS, int K, int LOOK, bool FOLD, typename W>
 __device__ __forceinline__ void inv_stages(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                           const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale) {
+                                           const Tw<W> *__restrict__ tw, const Arith<W> &ar, Scale<W> scale) {
     if constexpr (K >= 0) {
         if constexpr (K - LOOK >= 0) load_tw<LOGN, PASS, W, K - LOOK, K - LOOK + 1>(tau, tw, t);
         inv_stage<LOGN, PASS, K, FOLD>(v, t, ar, scale);
@@ -530,7 +530,7 @@ __device__ __forceinline__ void stream_begin(uint32_t tau, const Tw<W> *__restri
 // stream).
 template <int LOGN, int PASS, bool LAZY, bool RS, bool D2 = false, int I = 0, typename W>
 __device__ __forceinline__ void fwd_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&b)[PassTw<LOGN, PASS>::COUNT],
-                                                const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> rmod = Tw<W>{},
+                                                const Tw<W> *__restrict__ tw, const Arith<W> &ar, Scale<W> rmod = Scale<W>{},
                                                 W (*v2)[Geo<LOGN>::E] = nullptr) {
     using P = PassTw<LOGN, PASS>;
     constexpr int R = P::R;
@@ -558,7 +558,7 @@ __device__ __forceinline__ void fwd_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::
 // Inverse pass over the stream; FOLD: global stage 0 applies `scale`.
 template <int LOGN, int PASS, bool FOLD, bool D2 = false, int I = 0, typename W>
 __device__ __forceinline__ void inv_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::E], Tw<W> (&b)[PassTw<LOGN, PASS>::COUNT],
-                                                const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale,
+                                                const Tw<W> *__restrict__ tw, const Arith<W> &ar, Scale<W> scale,
                                                 W (*v2)[Geo<LOGN>::E] = nullptr) {
     using P = PassTw<LOGN, PASS>;
     constexpr int R = P::R;
@@ -648,7 +648,7 @@ __device__ __forceinline__ void fwd_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
             exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
             __syncthreads();
             exchange<LOGN, PASS - 1, PASS>(lds, v2, tau);
-            fwd_pass_stream<LOGN, PASS, LAZY, false, true>(tau, v, t, tw, ar, Tw<W>{}, &v2);
+            fwd_pass_stream<LOGN, PASS, LAZY, false, true>(tau, v, t, tw, ar, Scale<W>{}, &v2);
             fwd_rest2<LOGN, PASS + 1, LAZY, PF>(lds, v, v2, tau, tw, ar);
             return;
         }
@@ -664,7 +664,7 @@ __device__ __forceinline__ void fwd_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
 // Passes PASS..0 of the inverse transform (PASS+1 already in registers).
 template <int LOGN, int PASS, bool FOLD, int PF, typename W>
 __device__ __forceinline__ void inv_rest(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, const Tw<W> *__restrict__ tw,
-                                         const Arith<W> &ar, Tw<W> scale) {
+                                         const Arith<W> &ar, Scale<W> scale) {
     if constexpr (PASS >= 0) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
         if constexpr (stream_tw<LOGN, W>()) {
@@ -698,8 +698,13 @@ struct NttArgs {
     const Tw<W> *twi;      // inverse stage table
     Arith<W> ar;
     uint64_t q64, mu64;    // exact slow-path reduction of out-of-range inputs
-    Tw<W> ninv;            // N^-1
-    Tw<W> ninv_r;          // N^-1 * R  (after a Montgomery pointwise product)
+    // Stage-0 multipliers (Scale): the inverse folds N^-1 into its last GS
+    // stage and the R-scaled forward multiplies by R in its first CT stage,
+    // each in place of that stage's twiddle w0 -- 1 in compat mode, psi^(N/2)
+    // in negacyclic mode (merged stage tables), so .b carries w0 (or w0^-1).
+    Scale<W> ninv;         // {N^-1, N^-1 w0^-1}
+    Scale<W> ninv_r;       // {N^-1 R, N^-1 R w0^-1}  (after a Montgomery pointwise product)
+    Scale<W> rs;           // {R, R w0}  (fwd * R, Montgomery form)
     Tw<W> rmod;            // R mod q  (to Montgomery form)
     Tw<W> one;             // {1, floor(2^W / q)}: shoup(x, one) = x mod q in [0, 2q)
 };
@@ -868,9 +873,9 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
     }
     if constexpr (ST) {
         stream_begin<LOGN, 0, false, RS>(tau, A.twf, t0);
-        fwd_pass_stream<LOGN, 0, LAZY, RS>(tau, v, t0, A.twf, A.ar, A.rmod);
+        fwd_pass_stream<LOGN, 0, LAZY, RS>(tau, v, t0, A.twf, A.ar, A.rs);
     } else {
-        fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rmod);
+        fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rs);
     }
     fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar, hook);
 }
@@ -902,7 +907,7 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     }
     if constexpr (ST) {
         stream_begin<LOGN, 0, false, false>(tau, A.twf, t0);
-        fwd_pass_stream<LOGN, 0, LAZY, false, true>(tau, v, t0, A.twf, A.ar, Tw<W>{}, &v2);
+        fwd_pass_stream<LOGN, 0, LAZY, false, true>(tau, v, t0, A.twf, A.ar, Scale<W>{}, &v2);
     } else {
         fwd_pass<LOGN, 0, LAZY, W>(v, t0, A.ar);
         fwd_pass<LOGN, 0, LAZY, W>(v2, t0, A.ar);
@@ -922,7 +927,7 @@ struct NoFin {
 // STORE = false: fin() does every store itself (dst unused).
 template <int LOGN, int PF = kPfSingle, bool STORE = true, typename W, typename F = NoFin>
 __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau, uint64_t *__restrict__ dst,
-                                                   bool valid, const NttArgs<W> &A, Tw<W> scale, uint32_t sh = 0,
+                                                   bool valid, const NttArgs<W> &A, Scale<W> scale, uint32_t sh = 0,
                                                    F &&fin = NoFin{}) {
     using G = Geo<LOGN>;
     constexpr int LAST = G::NP - 1;
@@ -956,7 +961,7 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
 template <int LOGN, int PASS, int K, int LOOK, bool FOLD, typename W>
 __device__ __forceinline__ void inv_stages2(uint32_t tau, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E],
                                             Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT], const Tw<W> *__restrict__ tw,
-                                            const Arith<W> &ar, Tw<W> scale) {
+                                            const Arith<W> &ar, Scale<W> scale) {
     if constexpr (K >= 0) {
         if constexpr (K - LOOK >= 0) load_tw<LOGN, PASS, W, K - LOOK, K - LOOK + 1>(tau, tw, t);
         inv_stage<LOGN, PASS, K, FOLD>(v, t, ar, scale);
@@ -967,7 +972,7 @@ __device__ __forceinline__ void inv_stages2(uint32_t tau, W (&v)[Geo<LOGN>::E], 
 }
 template <int LOGN, int PASS, bool FOLD, int PF, typename W>
 __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
-                                          const Tw<W> *__restrict__ tw, const Arith<W> &ar, Tw<W> scale) {
+                                          const Tw<W> *__restrict__ tw, const Arith<W> &ar, Scale<W> scale) {
     if constexpr (PASS >= 0) {
         Tw<W> t[PassTw<LOGN, PASS>::COUNT];
         if constexpr (stream_tw2<LOGN, W>()) {
@@ -992,7 +997,7 @@ __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
 template <int LOGN, int PF, typename W, typename F1 = NoFin, typename F2 = NoFin>
 __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[Geo<LOGN>::E], uint32_t tau,
                                           uint64_t *__restrict__ dst, uint64_t *__restrict__ dst2,
-                                          const NttArgs<W> &A, Tw<W> scale, F1 &&fin1 = NoFin{}, F2 &&fin2 = NoFin{}) {
+                                          const NttArgs<W> &A, Scale<W> scale, F1 &&fin1 = NoFin{}, F2 &&fin2 = NoFin{}) {
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
     constexpr int LAST = G::NP - 1;
