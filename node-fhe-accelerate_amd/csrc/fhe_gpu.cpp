@@ -1727,6 +1727,18 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
     FHE_TRY(hs.map(where, bsk_ntt, ggsw_words * lwe_dim * 8, 1));
     FHE_TRY(hs.map(where, acc, bytes, 3));
     static const bool no_graph = std::getenv("FHE_NO_GRAPH") && std::getenv("FHE_NO_GRAPH")[0] == '1';
+    // The whole loop as one launch with the accumulators in LDS
+    // (ntt_br.hip; k = 1 and k = 2 at small N); FHE_BR_PERSIST_MAX caps the
+    // batch it takes (0 = never).
+    const char *pm = std::getenv("FHE_BR_PERSIST_MAX");
+    const size_t persist_max = pm ? (size_t)std::strtoull(pm, nullptr, 10) : kBrPersistMax;
+    if (lwe_dim > 0 && batch <= persist_max && (int)c->logn <= FHE_NS::kMaxFusedLogN &&
+        FHE_NS::br_persist_supported(c->plan, (int)k + 1)) {
+        HIP_TRY(FHE_NS::launch_br_persist(c->plan, (int)k + 1, (int)level, (int)base_log, acc, bsk_ntt, lwe_a, lwe_b,
+                                          lwe_dim, lwe_q, batch),
+                "blind rotate kernel");
+        return where == FHE_HOST ? hs.finish() : FHE_OK;
+    }
     const bool composed = !fused_tfhe(c, k);
     // composed steps (k > 1, N > 16384, q >= 2^62): six launches per CMux;
     // device-resident calls with fused transforms are captured into the
@@ -1735,16 +1747,6 @@ int fhe_blind_rotate_batch(fhe_ctx *c, uint32_t k, uint32_t base_log, uint32_t l
                                 (int)c->logn <= FHE_NS::kMaxFusedLogN;
     if (composed && !composed_graph) {
         FHE_TRY(blind_rotate_composed(c, k, base_log, level, lwe_dim, lwe_a, lwe_b, lwe_q, bsk_ntt, acc, batch));
-        return where == FHE_HOST ? hs.finish() : FHE_OK;
-    }
-    // The whole loop as one launch with the accumulators in LDS
-    // (ntt_br.hip); FHE_BR_PERSIST_MAX caps the batch it takes (0 = never).
-    const char *pm = std::getenv("FHE_BR_PERSIST_MAX");
-    const size_t persist_max = pm ? (size_t)std::strtoull(pm, nullptr, 10) : kBrPersistMax;
-    if (!composed && lwe_dim > 0 && batch <= persist_max && FHE_NS::br_persist_supported(c->plan, (int)k + 1)) {
-        HIP_TRY(FHE_NS::launch_br_persist(c->plan, (int)k + 1, (int)level, (int)base_log, acc, bsk_ntt, lwe_a, lwe_b,
-                                          lwe_dim, lwe_q, batch),
-                "blind rotate kernel");
         return where == FHE_HOST ? hs.finish() : FHE_OK;
     }
     std::lock_guard<std::mutex> lk(c->br_mu);

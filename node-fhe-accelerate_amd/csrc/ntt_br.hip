@@ -130,19 +130,151 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
     for (uint32_t i = threadIdx.x; i < 2u * N; i += G::THREADS) gacc[i] = accs[i / N][i % N];
 }
 
-bool br_persist_supported(const Plan &p, int k1) { return k1 == 2 && p.logn >= 9 && p.logn <= 11; }
+// GLWE dimension k >= 2 (K1 = k + 1 >= 3 accumulators): the same one-launch
+// structure, generic in K1.  A step has K1 L digit rows; the two 128-thread
+// halves transform them two at a time (row r0 + half), and every row's
+// product with the step's GGSW goes to all K1 output components, so each
+// half accumulates its rows' contributions for all K1 components in its own
+// NTT-domain LDS region (oacc[half][j], own positions: no barrier).  The K1
+// inverses then run two at a time, each from the sum of the two halves'
+// partials, and their epilogue adds the old accumulator (cmux :537).  Rows
+// and components past the end leave that half idle for the round (it still
+// runs the transform on zeros: the exchange barriers are workgroup-wide).
+template <int LOGN, typename W, int K1>
+constexpr int br_k_lds_bytes() {
+    using G = Geo<br_key<LOGN>()>;
+    return K1 * G::N * 8 + 2 * G::LW * (int)sizeof(W) + 2 * K1 * G::N * (int)sizeof(W);
+}
+template <int LOGN, typename W, int K1>
+__global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
+    constexpr int K = br_key<LOGN>();
+    using G = Geo<K>;
+    static_assert(G::P == 2 && G::THREADS == 256, "two 128-thread halves per workgroup");
+    static_assert(br_k_lds_bytes<LOGN, W, K1>() <= 160 * 1024, "LDS");
+    constexpr int N = G::N;
+    __shared__ uint64_t accs[K1][N];   // raw accumulators (component j)
+    __shared__ W xlds[2 * G::LW];      // NTT exchange, one region per half
+    __shared__ W oacc[2][K1][N];       // NTT-domain partial sums per half
+    const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
+    const size_t ct = blockIdx.x;
+    const uint64_t q = A.q64, mu = A.mu64;
+    W *lds = xlds + pl * G::LW;
+    uint64_t *gacc = D.acc + ct * K1 * N;
+    {
+        const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(K1 * N); i += G::THREADS) {
+            const uint32_t j = i / N, p = i % N;
+            accs[j][p] = rotated_at(gacc + (size_t)j * N, p, r0, N, q, mu);
+        }
+    }
+    __syncthreads();
+    const int level = D.level, rows = K1 * level;
+    const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    const size_t ggsw_words = (size_t)rows * K1 * N;
+    const uint64_t *lwe_a = D.lwe_a + ct * D.lwe_dim;
+    for (uint32_t step = 0; step < D.lwe_dim; ++step) {
+        const int32_t r = rot_amount(lwe_a[step], N, D.lwe_q);  // workgroup-uniform
+        if (r == 0) continue;
+        const uint32_t rot = rot_norm(r, N);
+        const uint64_t *key = D.bsk + ggsw_words * step;
+        for (int rb = 0; rb < rows; rb += 2) {
+            const int row = rb + (int)pl;
+            const bool active = row < rows;
+            const int comp = active ? row / level : 0, g = active ? row % level : 0;
+            const uint32_t shift = uint32_t(level - 1 - g) * uint32_t(D.base_log);
+            uint32_t tr = tau;
+            asm volatile("" : "+v"(tr));
+            // this row's key terms for all K1 components, in flight across
+            // the transform (issued first: loads retire in order)
+            const uint64_t *kr = key + (size_t)(active ? row : 0) * K1 * N;
+            uint64_t kv[K1][G::E];
+#pragma unroll
+            for (int j = 0; j < K1; ++j)
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) kv[j][e] = kr[(size_t)j * N + gidx<K, G::NP - 1>(tr, e)];
+            W v[G::E];
+            Tw<W> t0[PassTw<K, 0>::COUNT];
+            load_tw<K, 0>(tr, A.twf, t0);
+            const uint64_t *ac = accs[comp];
+            load_coeffs<G::E>(v, (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
+                if (!active) return 0;
+                const uint32_t p = tr + cbrv(t, G::LOGE) * G::T;
+                const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
+                const uint64_t xr = j < (uint32_t)N ? ac[j] : red_q(q - ac[j - N], q, mu);
+                const uint64_t c = subq(red_q(xr, q, mu), red_q(ac[p], q, mu), q);
+                uint64_t d = (c >> shift) & mask;
+                if (d > half) d = red_q(q - (base - d), q, mu);
+                return d;
+            });
+            fwd_pass<K, 0, false>(v, t0, A.ar);
+            fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
+            if (active) {
+                // raw output (< 4q) times canonical keys: valid Montgomery pairs
+#pragma unroll
+                for (int j = 0; j < K1; ++j) {
+#pragma unroll
+                    for (int e = 0; e < G::E; ++e) {
+                        const uint32_t gi = gidx<K, G::NP - 1>(tr, e);
+                        const W m = A.ar.mont(v[e], (W)kv[j][e]);
+                        oacc[pl][j][gi] = rb < 2 ? m : A.ar.red2q(oacc[pl][j][gi] + m);
+                    }
+                }
+            }
+            __syncthreads();  // the exchange regions are reused by the next round
+        }
+        // components j0 + pl: inverse of the two halves' sum, then
+        // acc_j = mod_add(inv, red_q(acc_j))
+        for (int j0 = 0; j0 < K1; j0 += 2) {
+            const int j = j0 + (int)pl;
+            const bool active = j < K1;
+            uint32_t ti = tau;
+            asm volatile("" : "+v"(ti));
+            W v[G::E];
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const uint32_t gi = gidx<K, G::NP - 1>(ti, e);
+                v[e] = active ? A.ar.red2q(oacc[0][j][gi] + oacc[1][j][gi]) : W(0);
+            }
+            uint64_t *ap = accs[active ? j : 0];
+            inv_poly_from_regs<K, kPfSingle, false>(lds, v, ti, nullptr, true, A, A.ninv, 0,
+                                                    [&](uint32_t gi, uint64_t x) -> uint64_t {
+                                                        if (active) ap[gi] = addq(x, red_q(ap[gi], q, mu), q);
+                                                        return 0;
+                                                    });
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(K1 * N); i += G::THREADS) gacc[i] = accs[i / N][i % N];
+}
+
+// k1 == 2: N = 512..2048; k1 == 3 (GLWE dimension 2): N = 512 / 1024 (and
+// 2048 with 32-bit words), where the K1 accumulators and both halves'
+// partial sums fit in LDS.
+bool br_persist_supported(const Plan &p, int k1) {
+    if (p.wide) return false;
+    if (k1 == 2) return p.logn >= 9 && p.logn <= 11;
+    if (k1 == 3) return p.logn >= 9 && (p.logn <= 10 || (p.logn == 11 && p.word == 32));
+    return false;
+}
 
 template <int LOGN, typename W>
-static hipError_t br_one(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
-    hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+static hipError_t br_one(const Plan &p, int k1, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
+    if (k1 == 2) {
+        hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+    } else {
+        if constexpr (br_k_lds_bytes<LOGN, W, 3>() <= 160 * 1024)
+            hipLaunchKernelGGL((k_br_persist_k<LOGN, W, 3>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+        else
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 template <typename W>
-static hipError_t br_dispatch(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
+static hipError_t br_dispatch(const Plan &p, int k1, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
     switch (p.logn) {
-    case 9: return br_one<9, W>(p, D, batch, A);
-    case 10: return br_one<10, W>(p, D, batch, A);
-    case 11: return br_one<11, W>(p, D, batch, A);
+    case 9: return br_one<9, W>(p, k1, D, batch, A);
+    case 10: return br_one<10, W>(p, k1, D, batch, A);
+    case 11: return br_one<11, W>(p, k1, D, batch, A);
     default: return hipErrorInvalidValue;
     }
 }
@@ -156,10 +288,10 @@ hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uin
     const size_t per = (size_t)1 << 30;
     for (size_t b0 = 0; b0 < batch; b0 += per) {
         const size_t nb = batch - b0 < per ? batch - b0 : per;
-        BrArgs D{acc + b0 * 2 * ((size_t)1 << p.logn), bsk, lwe_a + b0 * lwe_dim, lwe_b + b0, lwe_q, lwe_dim, level,
-                 base_log};
-        hipError_t e = p.word == 32 ? br_dispatch<uint32_t>(p, D, nb, p.a32)
-                                    : br_dispatch<uint64_t>(p, D, nb, p.a64);
+        BrArgs D{acc + b0 * (size_t)k1 * ((size_t)1 << p.logn), bsk, lwe_a + b0 * lwe_dim, lwe_b + b0, lwe_q, lwe_dim,
+                 level, base_log};
+        hipError_t e = p.word == 32 ? br_dispatch<uint32_t>(p, k1, D, nb, p.a32)
+                                    : br_dispatch<uint64_t>(p, k1, D, nb, p.a64);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

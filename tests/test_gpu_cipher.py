@@ -179,15 +179,18 @@ def test_blind_rotate_vs_oracle(fg, n, q, bl, lv, dim):
         assert (acc[i] == exp).all(), i
 
 
-@pytest.mark.parametrize("n,q,bl,lv,mode", [(512, 12289, 4, 3, "compat"), (1024, P62, 23, 1, "compat"),
-                                            (1024, P27, 9, 3, "negacyclic"), (1024, P62, 15, 2, "negacyclic"),
-                                            (2048, P62, 23, 1, "compat"), (2048, 40961, 5, 2, "compat")])
-def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q, bl, lv, mode):
+@pytest.mark.parametrize("n,q,bl,lv,mode,k", [(512, 12289, 4, 3, "compat", 1), (1024, P62, 23, 1, "compat", 1),
+                                              (1024, P27, 9, 3, "negacyclic", 1), (1024, P62, 15, 2, "negacyclic", 1),
+                                              (2048, P62, 23, 1, "compat", 1), (2048, 40961, 5, 2, "compat", 1),
+                                              (512, 12289, 4, 3, "compat", 2), (1024, P62, 15, 2, "compat", 2),
+                                              (1024, P27, 9, 3, "negacyclic", 2), (2048, 40961, 5, 2, "compat", 2)])
+def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q, bl, lv, mode, k):
     """Small batches take the single-launch blind rotation (ntt_br.hip,
-    accumulators in LDS for the whole loop); FHE_BR_PERSIST_MAX=0 forces the
-    per-step launches.  Both bit-exact with each other, and rows vs the
-    oracle (compat mode)."""
-    k, b, dim = 1, 5, 24
+    accumulators in LDS for the whole loop; k = 1 and, with K1 = 3
+    accumulators, k = 2); FHE_BR_PERSIST_MAX=0 forces the per-step launches
+    (k = 1) or the composed steps (k = 2).  Both bit-exact with each other,
+    and rows vs the oracle (compat mode)."""
+    b, dim = 5, 24
     r = fg.PolynomialRing(n, q, mode=mode)
     be = fg.BootstrapEngine(r, bl, lv, k)
     bsk = rnd(71 + n, q, dim, (k + 1) * lv, k + 1, n)
