@@ -131,30 +131,38 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
 }
 
 // GLWE dimension k >= 2 (K1 = k + 1 >= 3 accumulators): the same one-launch
-// structure, generic in K1.  A step has K1 L digit rows; the two 128-thread
-// halves transform them two at a time (row r0 + half), and every row's
-// product with the step's GGSW goes to all K1 output components, so each
-// half accumulates its rows' contributions for all K1 components in its own
-// NTT-domain LDS region (oacc[half][j], own positions: no barrier).  The K1
-// inverses then run two at a time, each from the sum of the two halves'
+// structure, generic in K1.  A step has K1 L digit rows; P thread groups
+// transform them P at a time (row r0 + group), and every row's product with
+// the step's GGSW goes to all K1 output components, so each group
+// accumulates its rows' contributions for all K1 components in its own
+// NTT-domain LDS region (oacc[group][j], own positions: no barrier).  The
+// K1 inverses then run P at a time, each from the sum of the groups'
 // partials, and their epilogue adds the old accumulator (cmux :537).  Rows
-// and components past the end leave that half idle for the round (it still
+// and components past the end leave that group idle for the round (it still
 // runs the transform on zeros: the exchange barriers are workgroup-wide).
-template <int LOGN, typename W, int K1>
+// 2^LOGP transforms at a time (groups of 256 >> LOGP threads): 4 where the
+// four groups' partial sums fit in LDS (fewer, longer rounds: 2 forward and
+// 1 inverse round per step at K1 L = 6 instead of 3 and 2), else 2.
+template <int LOGN, int LOGP>
+constexpr int br_k_key() { return gk(LOGN, LOGN - 8 + LOGP); }
+template <int LOGN, typename W, int K1, int LOGP>
 constexpr int br_k_lds_bytes() {
-    using G = Geo<br_key<LOGN>()>;
-    return K1 * G::N * 8 + 2 * G::LW * (int)sizeof(W) + 2 * K1 * G::N * (int)sizeof(W);
+    using G = Geo<br_k_key<LOGN, LOGP>()>;
+    return K1 * G::N * 8 + (1 << LOGP) * G::LW * (int)sizeof(W) + (1 << LOGP) * K1 * G::N * (int)sizeof(W);
 }
 template <int LOGN, typename W, int K1>
+constexpr int br_k_logp() { return br_k_lds_bytes<LOGN, W, K1, 2>() <= 160 * 1024 ? 2 : 1; }
+template <int LOGN, typename W, int K1, int LOGP>
 __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
-    constexpr int K = br_key<LOGN>();
+    constexpr int K = br_k_key<LOGN, LOGP>();
     using G = Geo<K>;
-    static_assert(G::P == 2 && G::THREADS == 256, "two 128-thread halves per workgroup");
-    static_assert(br_k_lds_bytes<LOGN, W, K1>() <= 160 * 1024, "LDS");
+    constexpr int P = 1 << LOGP;
+    static_assert(G::P == P && G::THREADS == 256, "P thread groups per workgroup");
+    static_assert(br_k_lds_bytes<LOGN, W, K1, LOGP>() <= 160 * 1024, "LDS");
     constexpr int N = G::N;
     __shared__ uint64_t accs[K1][N];   // raw accumulators (component j)
-    __shared__ W xlds[2 * G::LW];      // NTT exchange, one region per half
-    __shared__ W oacc[2][K1][N];       // NTT-domain partial sums per half
+    __shared__ W xlds[P * G::LW];      // NTT exchange, one region per group
+    __shared__ W oacc[P][K1][N];       // NTT-domain partial sums per group
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t ct = blockIdx.x;
     const uint64_t q = A.q64, mu = A.mu64;
@@ -177,7 +185,7 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
         if (r == 0) continue;
         const uint32_t rot = rot_norm(r, N);
         const uint64_t *key = D.bsk + ggsw_words * step;
-        for (int rb = 0; rb < rows; rb += 2) {
+        for (int rb = 0; rb < rows; rb += P) {
             const int row = rb + (int)pl;
             const bool active = row < rows;
             const int comp = active ? row / level : 0, g = active ? row % level : 0;
@@ -216,7 +224,7 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
                     for (int e = 0; e < G::E; ++e) {
                         const uint32_t gi = gidx<K, G::NP - 1>(tr, e);
                         const W m = A.ar.mont(v[e], (W)kv[j][e]);
-                        oacc[pl][j][gi] = rb < 2 ? m : A.ar.red2q(oacc[pl][j][gi] + m);
+                        oacc[pl][j][gi] = rb < P ? m : A.ar.red2q(oacc[pl][j][gi] + m);
                     }
                 }
             }
@@ -224,7 +232,7 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
         }
         // components j0 + pl: inverse of the two halves' sum, then
         // acc_j = mod_add(inv, red_q(acc_j))
-        for (int j0 = 0; j0 < K1; j0 += 2) {
+        for (int j0 = 0; j0 < K1; j0 += P) {
             const int j = j0 + (int)pl;
             const bool active = j < K1;
             uint32_t ti = tau;
@@ -233,7 +241,14 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
 #pragma unroll
             for (int e = 0; e < G::E; ++e) {
                 const uint32_t gi = gidx<K, G::NP - 1>(ti, e);
-                v[e] = active ? A.ar.red2q(oacc[0][j][gi] + oacc[1][j][gi]) : W(0);
+                W x = 0;
+                if (active) {
+                    // groups that ran no row of this step hold stale partials
+#pragma unroll
+                    for (int h = 0; h < P; ++h)
+                        if (h < rows) x = A.ar.red2q(x + oacc[h][j][gi]);
+                }
+                v[e] = x;
             }
             uint64_t *ap = accs[active ? j : 0];
             inv_poly_from_regs<K, kPfSingle, false>(lds, v, ti, nullptr, true, A, A.ninv, 0,
@@ -262,8 +277,9 @@ static hipError_t br_one(const Plan &p, int k1, const BrArgs &D, size_t batch, c
     if (k1 == 2) {
         hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
     } else {
-        if constexpr (br_k_lds_bytes<LOGN, W, 3>() <= 160 * 1024)
-            hipLaunchKernelGGL((k_br_persist_k<LOGN, W, 3>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+        constexpr int LP = br_k_logp<LOGN, W, 3>();
+        if constexpr (br_k_lds_bytes<LOGN, W, 3, LP>() <= 160 * 1024)
+            hipLaunchKernelGGL((k_br_persist_k<LOGN, W, 3, LP>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
         else
             return hipErrorInvalidValue;
     }
