@@ -140,9 +140,14 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
 // partials, and their epilogue adds the old accumulator (cmux :537).  Rows
 // and components past the end leave that group idle for the round (it still
 // runs the transform on zeros: the exchange barriers are workgroup-wide).
-// 2^LOGP transforms at a time (groups of 256 >> LOGP threads): 4 where the
-// four groups' partial sums fit in LDS (fewer, longer rounds: 2 forward and
-// 1 inverse round per step at K1 L = 6 instead of 3 and 2), else 2.
+// 2^LOGP transforms at a time (groups of 256 >> LOGP threads).  Four groups
+// (fewer, longer rounds: 2 forward and 1 inverse round per step at K1 L = 6
+// instead of 3 and 2) measured slower on MI355X -- 25.2 vs 20.1 ms for one
+// k = 2, N = 1024 blind rotation (profiles/r3j) -- so two (FHE_BRK_P4=1
+// keeps the four-group build for A/B).
+#ifndef FHE_BRK_P4
+#define FHE_BRK_P4 0
+#endif
 template <int LOGN, int LOGP>
 constexpr int br_k_key() { return gk(LOGN, LOGN - 8 + LOGP); }
 template <int LOGN, typename W, int K1, int LOGP>
@@ -151,7 +156,11 @@ constexpr int br_k_lds_bytes() {
     return K1 * G::N * 8 + (1 << LOGP) * G::LW * (int)sizeof(W) + (1 << LOGP) * K1 * G::N * (int)sizeof(W);
 }
 template <int LOGN, typename W, int K1>
-constexpr int br_k_logp() { return br_k_lds_bytes<LOGN, W, K1, 2>() <= 160 * 1024 ? 2 : 1; }
+constexpr int br_k_logp() { return FHE_BRK_P4 && br_k_lds_bytes<LOGN, W, K1, 2>() <= 160 * 1024 ? 2 : 1; }
+// twiddle stages issued ahead in the k >= 2 kernel's transforms
+#ifndef FHE_BRK_PF
+#define FHE_BRK_PF 4
+#endif
 template <int LOGN, typename W, int K1, int LOGP>
 __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
     constexpr int K = br_k_key<LOGN, LOGP>();
@@ -215,7 +224,7 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
                 return d;
             });
             fwd_pass<K, 0, false>(v, t0, A.ar);
-            fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
+            fwd_rest<K, 1, false, FHE_BRK_PF>(lds, v, tr, A.twf, A.ar);
             if (active) {
                 // raw output (< 4q) times canonical keys: valid Montgomery pairs
 #pragma unroll
@@ -251,9 +260,9 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
                 v[e] = x;
             }
             uint64_t *ap = accs[active ? j : 0];
-            inv_poly_from_regs<K, kPfSingle, false>(lds, v, ti, nullptr, true, A, A.ninv, 0,
-                                                    [&](uint32_t gi, uint64_t x) -> uint64_t {
-                                                        if (active) ap[gi] = addq(x, red_q(ap[gi], q, mu), q);
+            inv_poly_from_regs<K, FHE_BRK_PF, false>(lds, v, ti, nullptr, true, A, A.ninv, 0,
+                                                     [&](uint32_t gi, uint64_t x) -> uint64_t {
+                                                         if (active) ap[gi] = addq(x, red_q(ap[gi], q, mu), q);
                                                         return 0;
                                                     });
             __syncthreads();
