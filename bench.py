@@ -424,8 +424,15 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
             ggsw = torch.randint(0, q, (2 * lv, 2, n), device="cuda", dtype=torch.int64, generator=g)
             ep = fhe_gpu.ExternalProduct(ring, ggsw, bl, lv)
             wall, kms = timed(dist, lambda: ep(glwe, out=out), steps, warmup)
+            alg = 32 * n * B  # the GLWE in and out; the GGSW rows are shared by the batch (L2)
             c5[f"extprod_B{bl}_L{lv}"] = {"per_s": B * steps / wall, "kernel_ms": kms,
-                                          "transforms_per_unit": 2 * lv + 2}
+                                          "transforms_per_unit": 2 * lv + 2,
+                                          "algorithmic_bytes_per_launch": alg,
+                                          "achieved_GBs": alg / (kms * 1e-3) / 1e9}
+            tr = side_traffic("k_extprod_acc<" if lv > 1 else "k_extprod2<14, unsigned long>", B)
+            if tr:
+                c5[f"extprod_B{bl}_L{lv}"].update(traffic=tr[0], traffic_source=tr[1],
+                                                  traffic_over_algorithmic=tr[0] / alg)
         del glwe, out
         cnt = 16384 * 1024
         ml = fhe_gpu.MultiLimbModularArithmetic([0xFFFFFFFF00000001, 0x3FFFFFFFFFFFFFFF])
@@ -507,6 +514,27 @@ def pmc_traffic(kernel, n, batch, q, mode="compat"):
         if not (w.get("kernel") == kernel and w.get("n") == n and w.get("batch") == batch and w.get("q") == q
                 and w.get("mode", "compat") == mode
                 and "hbm_traffic_bytes_per_launch" in s and sym in s.get("kernel_name", "")):
+            continue
+        key = (s.get("generated", ""), f)
+        if best is None or key > best[0]:
+            best = (key, s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best[1:] if best else None
+
+
+def side_traffic(kernel_prefix, batch):
+    """HBM bytes per launch of a side-metric kernel from the newest committed
+    rocprofv3 summary whose profiled kernel starts with `kernel_prefix`
+    (tools/gpu_prof_side.sh + summarize_profile.py); launches of the bench's
+    batch only (the summarizer keeps full-batch launches)."""
+    import glob
+
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
+        try:
+            s = json.load(open(f))
+        except Exception:
+            continue
+        if "hbm_traffic_bytes_per_launch" not in s or ("void fhe::" + kernel_prefix) not in s.get("kernel_name", ""):
             continue
         key = (s.get("generated", ""), f)
         if best is None or key > best[0]:
