@@ -299,10 +299,7 @@ def negacyclic_workload(fhe_gpu, n, q, batch, steps, warmup, dist):
         ach = 24 * n * batch / (kms * 1e-3) / 1e9
         out[key] = {"per_s": batch * steps / wall, "kernel_ms": kms, "achieved_GBs": ach,
                     "frac": ach / HBM_PEAK_GBS, "bytes_per_unit": 24 * n}
-        tr = pmc_traffic(key, n, batch, q, mode="negacyclic")
-        if tr:
-            out[key]["traffic"], out[key]["traffic_source"] = tr
-            out[key]["traffic_over_algorithmic"] = tr[0] / (24 * n * batch)
+        _attach(out[key], pmc_traffic(key, n, batch, q, mode="negacyclic"), 24 * n * batch)
     return out
 
 
@@ -400,6 +397,8 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
             res["ct_multiply"] = {"n": n, "q": q, "batch": B, "per_s": B * steps / wall, "kernel_ms": kms,
                                   "transforms_per_unit": 7, "bytes_per_unit": 56 * n,
                                   "achieved_GBs": 56 * n * B / (kms * 1e-3) / 1e9}
+            _attach(res["ct_multiply"], profile_traffic("ct_multiply", {"kernel": "ct_mul", "n": n, "batch": B, "q": q}),
+                    56 * n * B)
         if only in ("", "relin"):
             ek = fhe_gpu.EvaluationKey(ring, torch.randint(0, q, (lv, 2, n), device="cuda", dtype=torch.int64,
                                                            generator=g), bl)
@@ -409,6 +408,8 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
             res["relinearize"] = {"n": n, "q": q, "batch": B, "base_log": bl, "level": lv, "per_s": B * steps / wall,
                                   "kernel_ms": kms, "transforms_per_unit": lv + 2, "bytes_per_unit": 40 * n,
                                   "achieved_GBs": 40 * n * B / (kms * 1e-3) / 1e9}
+            _attach(res["relinearize"], profile_traffic("relinearize", {"kernel": "relin", "n": n, "batch": B, "q": q}),
+                    40 * n * B)
             del out, ek
         del x, y, ct3
     if only in ("", "c5"):
@@ -429,10 +430,7 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
                                           "transforms_per_unit": 2 * lv + 2,
                                           "algorithmic_bytes_per_launch": alg,
                                           "achieved_GBs": alg / (kms * 1e-3) / 1e9}
-            tr = side_traffic("k_extprod_acc<" if lv > 1 else "k_extprod2<14, unsigned long>", B)
-            if tr:
-                c5[f"extprod_B{bl}_L{lv}"].update(traffic=tr[0], traffic_source=tr[1],
-                                                  traffic_over_algorithmic=tr[0] / alg)
+            _attach(c5[f"extprod_B{bl}_L{lv}"], profile_traffic(f"extprod_B{bl}_L{lv}"), alg)
         del glwe, out
         cnt = 16384 * 1024
         ml = fhe_gpu.MultiLimbModularArithmetic([0xFFFFFFFF00000001, 0x3FFFFFFFFFFFFFFF])
@@ -484,62 +482,83 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
     return res
 
 
-KERNEL_SYMBOL = {"fwd_mul": "k_ntt_fwd_mul", "polymul": "k_polymul", "fwd": "k_ntt_fwd", "inv": "k_ntt_inv"}
+# The exact kernels this bench launches (the library's dispatch for these
+# shapes).  A PMC traffic figure is attached only from a profile summary of
+# that exact demangled symbol, measured on the library now loaded (same
+# fhe_build_id(): same sources, flags and code objects); anything else gives
+# traffic null.  tests/test_abi.py checks each symbol exists in the build.
+def _nargs(w):
+    return f"(unsigned long const*, unsigned long const*, unsigned long*, unsigned long, fhe::NttArgs<unsigned {w}>)"
+
+
+BENCH_KERNELS = {
+    "fwd_mul/q27": "void fhe::k_ntt_fwd_mul<14, unsigned int, true>" + _nargs("int"),
+    "polymul/q27": "void fhe::k_polymul2<1294, unsigned int, true>" + _nargs("int"),
+    "fwd_mul/q62": "void fhe::k_ntt_fwd_mul<1294, unsigned long, false>" + _nargs("long"),
+    "polymul/q62": "void fhe::k_polymul2<14, unsigned long, false>" + _nargs("long"),
+    "extprod_B23_L1": "void fhe::k_extprod2<14, unsigned long>(fhe::DmArgs, fhe::NttArgs<unsigned long>)",
+    "extprod_B15_L2": "void fhe::k_extprod_acc<1294>(fhe::ExtAccArgs, fhe::NttArgs<unsigned long>)",
+    "ct_multiply": "void fhe::k_ct_mul2<1294, unsigned int, true>" + _nargs("int"),
+    "relinearize": "void fhe::k_dmac<14, unsigned int, 2, false, 1>(fhe::DmArgs, fhe::NttArgs<unsigned int>)",
+}
+
+
+def _build_id():
+    try:
+        import fhe_gpu
+
+        return fhe_gpu.build_id()
+    except Exception:  # pragma: no cover
+        return None
+
+
+def profile_traffic(key, workload=None):
+    """(HBM bytes per launch, summary path, profiled kernel ms) from the
+    newest profiles/*/summary.json of kernel BENCH_KERNELS[key] stamped with
+    the loaded library's build id (and, when given, the same workload), or
+    None.  Written by tools/gpu_evidence.sh + tools/summarize_profile.py."""
+    import glob
+
+    sym, bid = BENCH_KERNELS[key], _build_id()
+    if bid is None:
+        return None
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
+        try:
+            s = json.load(open(f))
+        except Exception:
+            continue
+        if s.get("build_id") != bid or s.get("kernel_name") != sym or "hbm_traffic_bytes_per_launch" not in s:
+            continue
+        if workload is not None:
+            w = dict(s.get("workload", {}))
+            w.setdefault("mode", "compat")
+            if any(w.get(k) != v for k, v in workload.items()):
+                continue
+        key_ = (s.get("generated", ""), f)
+        if best is None or key_ > best[0]:
+            kt = s.get("kernel_trace_full_batch", {})
+            best = (key_, s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT),
+                    kt.get("avg_ns", 0) / 1e6 or None)
+    return best[1:] if best else None
 
 
 def pmc_traffic(kernel, n, batch, q, mode="compat"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of the
-    same workload (profiles/*/summary.json, tools/summarize_profile.py).
-    Only summaries whose profiled kernel is the template this run launches
-    (`k_<name><logN, word type`) count; among those the newest `generated`
-    stamp wins (summaries without one rank below every stamped one)."""
-    import glob
-
-    logn = n.bit_length() - 1
-    word = "unsigned int" if q < (1 << 30) else "unsigned long"
-    sym = f"{KERNEL_SYMBOL[kernel]}<{logn}, {word},"
-    if kernel == "polymul" and q < (1 << 30) and logn in (13, 14):
-        # 32 coefficients per thread, paired forward transforms (geometry key
-        # logN | 5 << 8; ntt_inv.hip k_polymul2)
-        sym = f"k_polymul2<{logn | (5 << 8)}, {word},"
-    elif kernel == "polymul" and q >= (1 << 30) and logn == 14:
-        sym = f"k_polymul2<{logn}, {word},"  # 64-bit words: paired, 16 per thread
-    best = None
-    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
-        try:
-            s = json.load(open(f))
-        except Exception:
-            continue
-        w = s.get("workload", {})
-        if not (w.get("kernel") == kernel and w.get("n") == n and w.get("batch") == batch and w.get("q") == q
-                and w.get("mode", "compat") == mode
-                and "hbm_traffic_bytes_per_launch" in s and sym in s.get("kernel_name", "")):
-            continue
-        key = (s.get("generated", ""), f)
-        if best is None or key > best[0]:
-            best = (key, s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
-    return best[1:] if best else None
+    """profile_traffic() of the headline kernels (fwd_mul / polymul)."""
+    if n != 16384 or kernel not in ("fwd_mul", "polymul") or q not in (P27, P62):
+        return None
+    key = f"{kernel}/{'q27' if q == P27 else 'q62'}"
+    return profile_traffic(key, {"kernel": kernel, "n": n, "batch": batch, "q": q, "mode": mode})
 
 
-def side_traffic(kernel_prefix, batch):
-    """HBM bytes per launch of a side-metric kernel from the newest committed
-    rocprofv3 summary whose profiled kernel starts with `kernel_prefix`
-    (tools/gpu_prof_side.sh + summarize_profile.py); launches of the bench's
-    batch only (the summarizer keeps full-batch launches)."""
-    import glob
-
-    best = None
-    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
-        try:
-            s = json.load(open(f))
-        except Exception:
-            continue
-        if "hbm_traffic_bytes_per_launch" not in s or ("void fhe::" + kernel_prefix) not in s.get("kernel_name", ""):
-            continue
-        key = (s.get("generated", ""), f)
-        if best is None or key > best[0]:
-            best = (key, s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
-    return best[1:] if best else None
+def _attach(d, tr, alg):
+    """Traffic fields of a roofline / side-metric record (null when unmatched)."""
+    if tr:
+        d["traffic"], d["traffic_source"], d["profile_kernel_ms"] = tr
+        d["traffic_over_algorithmic"] = tr[0] / alg
+    else:
+        d["traffic"] = None
+        d["traffic_source"] = "no profile of this exact kernel on this build (fhe_build_id)"
 
 
 def host_info():
@@ -632,10 +651,7 @@ def main():
                                  "frac": achp62 / HBM_PEAK_GBS},
         }
         for key, rl in (("fwd_mul", extra["q62"]["roofline"]), ("polymul", extra["q62"]["polymul_roofline"])):
-            tr = pmc_traffic(key, n, B, P62)
-            if tr:
-                rl["traffic"], rl["traffic_source"] = tr
-                rl["traffic_over_algorithmic"] = tr[0] / (24 * n * B)
+            _attach(rl, pmc_traffic(key, n, B, P62), 24 * n * B)
     if not args.only:
         nk = max(3, K // 4)
         extra["negacyclic"] = negacyclic_workload(fhe_gpu, n, args.q, B, nk, 1, dist)
@@ -678,11 +694,8 @@ def main():
                      "kernel": key, "kernel_ms": kms, "algorithmic_bytes_per_launch": bytes_per_unit * B},
         "parity_ok": r["parity_ok"],
     }
-    tr = pmc_traffic(key, n, B, args.q)
-    if tr:
-        line["roofline"]["traffic"] = tr[0]
-        line["roofline"]["traffic_source"] = tr[1]
-        line["roofline"]["traffic_over_algorithmic"] = tr[0] / (bytes_per_unit * B)
+    _attach(line["roofline"], pmc_traffic(key, n, B, args.q), bytes_per_unit * B)
+    line["build_id"] = _build_id()
     if "gather" in r:
         line["gather"] = r["gather"]
     if "polymul" in r:
@@ -691,10 +704,7 @@ def main():
         line["polymul_roofline"] = {"achieved": 24 * n * B / (pk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                     "unit": "GB/s", "kernel_ms": pk,
                                     "bound": "valu (3 transforms per 24N bytes; DESIGN.md section 6)"}
-        trp = pmc_traffic("polymul", n, B, args.q)
-        if trp:
-            line["polymul_roofline"]["traffic"] = trp[0]
-            line["polymul_roofline"]["traffic_source"] = trp[1]
+        _attach(line["polymul_roofline"], pmc_traffic("polymul", n, B, args.q), 24 * n * B)
     line.update(extra)
     if not args.no_cpu and world == 1 and not args.only:
         line["cpu_baseline"] = cpu_baseline(n, args.q, args.cpu_seconds)

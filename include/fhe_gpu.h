@@ -61,6 +61,11 @@ typedef struct fhe_ctx fhe_ctx;
 /* Thread-local message of the last failing call on this thread. */
 const char *fhe_last_error(void);
 const char *fhe_version(void);
+/* Hash of the sources and flags this library was built from (16 hex
+ * digits).  Profiles under profiles/ are stamped with it; bench.py uses a
+ * PMC traffic figure only when it matches the loaded library.  No reference
+ * counterpart (measurement plumbing). */
+const char *fhe_build_id(void);
 
 /* ---- hardware ------------------------------------------------------------
  * Replaces HardwareDetector::detect() (hardware_detector.mm; N-API
@@ -89,7 +94,13 @@ int fhe_detect(fhe_hw_caps *caps);
  * two-pass row/column split and the context holds 512 MiB of device
  * scratch (every entry point takes such contexts: fused kernels up to
  * n = 16384, composed ones above).
- * device: HIP device ordinal.                                              */
+ * device: HIP device ordinal.
+ * Side effect: call temporaries come from the device's default
+ * stream-ordered memory pool, and creating a context sets that pool's
+ * release threshold to FHE_POOL_KEEP_MB MiB (environment, default 8192), so
+ * up to that much freed memory stays cached across synchronisations.  The
+ * pool is process-wide (other HIP users of the device share it);
+ * FHE_POOL_KEEP_MB=0 leaves it unchanged.                                   */
 int fhe_ctx_create(uint32_t n, uint64_t q, int mode, int device, fhe_ctx **out);
 void fhe_ctx_destroy(fhe_ctx *ctx);
 /* Multi-device context (SURVEY.md 8(b) `devices, ndev`): one transform

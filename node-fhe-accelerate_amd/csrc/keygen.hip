@@ -101,6 +101,16 @@ __device__ uint64_t sample_one(int kind, Draws &d, uint64_t q, double std_dev) {
         const double smp = round(z * std_dev);
         int64_t v = (int64_t)smp;
         if (v < 0) {
+            if (q >> 63) {
+                // (int64_t)q = q - 2^64 < 0: the reference loop adds it until
+                // the sum wraps past INT64_MIN (signed overflow on its
+                // platform, ~2^31 iterations at q = 2^64 - 2^32 + 1).  The
+                // wrapped value in closed form: k = the first count with
+                // v - k m < -2^63 (m = 2^64 - q), result v - k m + 2^64.
+                const uint64_t m = 0ull - q;
+                const uint64_t k = ((uint64_t)(v + INT64_MAX) + 1) / m + 1;
+                return ((uint64_t)v - k * m) % q;
+            }
             v = (int64_t)q + v;
             while (v < 0) v += (int64_t)q;
         }

@@ -92,6 +92,7 @@ vp = C.c_void_p
 SIGNATURES = [
     ("fhe_last_error", C.c_char_p, []),
     ("fhe_version", C.c_char_p, []),
+    ("fhe_build_id", C.c_char_p, []),
     ("fhe_detect", C.c_int, [C.POINTER(HwCaps)]),
     ("fhe_ctx_create", C.c_int, [C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.POINTER(vp)]),
     ("fhe_ctx_destroy", None, [vp]),
@@ -206,6 +207,11 @@ def _check(rc: int):
 
 def version() -> str:
     return lib().fhe_version().decode()
+
+
+def build_id() -> str:
+    """Hash of the sources and flags of the loaded library (Makefile)."""
+    return lib().fhe_build_id().decode()
 
 
 def detect_hardware() -> dict:

@@ -621,6 +621,8 @@ struct job {
     char err[512];
     napi_ref refs[MAXP + 2];
     int nref;
+    dblock *blks[MAXP]; /* async path: device blocks pinned until completion */
+    int nblk;
     napi_ref ret;       /* async path */
     napi_deferred def;
     napi_async_work work;
@@ -636,6 +638,8 @@ typedef struct {
     int where;          /* -1 until the first buffer argument */
     size_t n;
     uint64_t q;
+    dblock *blks[MAXP]; /* device blocks of the buffer arguments (arr_arg) */
+    int nblk;
 } call;
 
 static int call_begin(napi_env env, napi_callback_info info, size_t want, call *k) {
@@ -644,6 +648,7 @@ static int call_begin(napi_env env, napi_callback_info info, size_t want, call *
     if (napi_get_cb_info(env, info, &k->argc, k->argv, &k->self, &data) != napi_ok) return -1;
     k->async = data != NULL;
     k->where = -1;
+    k->nblk = 0;
     k->k = unwrap_ctx(env, k->self);
     if (!k->k) {
         napi_throw_type_error(env, "INVALID_PARAMETERS", "not an NttContext");
@@ -669,6 +674,9 @@ static job *job_new(const call *k, job_fn fn, void *op) {
 
 static void job_free(napi_env env, job *j) {
     for (int i = 0; i < j->nref; ++i) napi_delete_reference(env, j->refs[i]);
+    /* after the job's final stream synchronisation: a buffer freed by the
+     * caller meanwhile is returned to the pool only now */
+    for (int i = 0; i < j->nblk; ++i) dblock_release(j->blks[i]);
     if (j->ret) napi_delete_reference(env, j->ret);
     free(j->owned);
     free(j);
@@ -717,6 +725,14 @@ static napi_value job_go(napi_env env, const call *k, job *j, napi_value ret, na
         return ret;
     }
     for (int i = 0; i < nkeep && j->nref < MAXP + 1; ++i) napi_create_reference(env, keep[i], 1, &j->refs[j->nref++]);
+    /* Each device block the job reads or writes is pinned by a block
+     * reference (not only its JS object): buf.free() while the job is queued
+     * must not let fhe_ctx_free enqueue the release ahead of the job's
+     * kernels, where a later allocation could reuse the memory. */
+    for (int i = 0; i < k->nblk; ++i) {
+        k->blks[i]->refs++;
+        j->blks[j->nblk++] = k->blks[i];
+    }
     napi_create_reference(env, k->self, 1, &j->refs[j->nref++]);
     napi_create_reference(env, ret, 1, &j->ret);
     napi_value promise, name;
@@ -743,6 +759,12 @@ static int arr_arg(napi_env env, call *k, size_t i, uint64_t **p, size_t *cnt) {
     dbuf *d = unwrap_buf(env, k->argv[i]);
     if (d) {
         if (!d->blk || d->blk->owner != k->k) return -1;
+        int seen = 0;
+        for (int b = 0; b < k->nblk; ++b) seen |= k->blks[b] == d->blk;
+        if (!seen) {
+            if (k->nblk >= MAXP) return -1;
+            k->blks[k->nblk++] = d->blk;
+        }
         *p = dbuf_ptr(d);
         *cnt = d->words;
         w = FHE_DEVICE;

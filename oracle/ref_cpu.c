@@ -822,6 +822,16 @@ void oracle_sample(int kind, const u64 seed[4], u64 stream, u64 q, double std_de
             while (u1 == 0.0) u1 = dr_unit(&d);
             const double z = sqrt(-2.0 * log(u1)) * cos(2.0 * 3.14159265358979323846 * u2);
             int64_t iv = (int64_t)round(z * std_dev);
+            if (iv < 0 && (q >> 63)) {
+                /* (int64_t)q < 0: the reference loop ends only when the sum
+                 * wraps past INT64_MIN (two's complement wrap, the AArch64
+                 * behaviour of its signed overflow); closed form of that
+                 * wrapped value (the loop would run ~2^31 times) */
+                const u64 m = 0ull - q;
+                const u64 k = ((u64)(iv + INT64_MAX) + 1) / m + 1;
+                v = ((u64)iv - k * m) % q;
+                break;
+            }
             if (iv < 0) { iv = (int64_t)q + iv; while (iv < 0) iv += (int64_t)q; }
             v = (u64)iv % q;
             break;

@@ -109,9 +109,15 @@ def ntt_large():
         i = t.inverse(x)
         m = t.polymul(x, y)
         fm = t.fwd_mul(x, y)
-        out.append({"n": n, "q": q, "batch": b, "seed_x": 0x5EED, "seed_y": 0xB0B,
-                    "sha_forward": sha(f), "sha_inverse": sha(i), "sha_polymul": sha(m), "sha_fwd_mul": sha(fm),
-                    "head_forward": L(f[0, :8]), "head_polymul": L(m[0, :8])})
+        e = {"n": n, "q": q, "batch": b, "seed_x": 0x5EED, "seed_y": 0xB0B,
+             "sha_forward": sha(f), "sha_inverse": sha(i), "sha_polymul": sha(m), "sha_fwd_mul": sha(fm),
+             "head_forward": L(f[0, :8]), "head_polymul": L(m[0, :8])}
+        if n >= 32768:
+            # two ciphertexts: rows (0, 1), (2, 3) of x times those of y
+            # (EncryptionEngine::multiply at the two-pass degrees)
+            ct = np.stack([t.ct_multiply(x[2 * j:2 * j + 2], y[2 * j:2 * j + 2]) for j in range(2)])
+            e["sha_ct_multiply"] = sha(ct)
+        out.append(e)
     return out
 
 

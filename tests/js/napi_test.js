@@ -207,6 +207,46 @@ if (mode === 'cpu') {
       assert.ok(ticks > before, 'event loop blocked while the async calls ran');
     }));
   });
+  test('concurrent async jobs on one N=32768 context (big-N scratch) vs golden', () => {
+    // forwardAsync and ctMultiplyAsync queued together on one NttContext:
+    // both stage host arrays through the context's big-N scratch
+    // (two-pass transforms, BigSync) and must not disturb each other
+    const c = goldenBig('ntt_large.json').find((x) => x.n === 32768 && BigInt(x.q) === 132120577n);
+    const n = c.n, q = BigInt(c.q);
+    const ctx = new fhe.NttContext(n, q);
+    const x = splitmix(c.seed_x, q, 4 * n), y = splitmix(c.seed_y, q, 4 * n);
+    const fx = x.slice();
+    const ct = new BigUint64Array(6 * n);
+    const fy = y.slice();
+    asyncTests.push(Promise.all([ctx.forwardAsync(fx), ctx.ctMultiplyAsync(x, y, ct), ctx.forwardAsync(fy)])
+      .then(() => {
+        assert.strictEqual(sha(fx), c.sha_forward, 'forward');
+        assert.strictEqual(sha(ct), c.sha_ct_multiply, 'ct multiply');
+        const fy2 = y.slice();
+        ctx.forward(fy2);
+        assert.deepStrictEqual(Array.from(fy), Array.from(fy2), 'second forward');
+      }));
+  });
+  test('DeviceBuffer freed while an async job that reads it is queued', () => {
+    // the job pins the block: the freed input must not be handed to the
+    // next allocation (and overwritten) before the queued job has read it
+    const c = goldenBig('ntt_large.json').find((x) => x.n === 16384 && BigInt(x.q) === 132120577n);
+    const n = c.n, q = BigInt(c.q);
+    const ctx = new fhe.NttContext(n, q);
+    const x = splitmix(c.seed_x, q, 4 * n);
+    const outs = [], pending = [];
+    for (let r = 0; r < 4; r++) {
+      const a = new fhe.DeviceBuffer(ctx, 4 * n).upload(x);
+      const out = new fhe.DeviceBuffer(ctx, 4 * n);
+      pending.push(ctx.forwardAsync(a, out));
+      a.free();
+      new fhe.DeviceBuffer(ctx, 4 * n).upload(new BigUint64Array(4 * n));  // would reuse a's memory
+      outs.push(out);
+    }
+    asyncTests.push(Promise.all(pending).then(() => {
+      for (const o of outs) assert.strictEqual(sha(o.download()), c.sha_forward);
+    }));
+  });
   test('multi-device NttContext splits host batches', () => {
     const hw = fhe.detectHardware();
     const devs = hw.gpuDevices > 1 ? [0, 1] : [0, 0];

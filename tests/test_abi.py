@@ -241,3 +241,30 @@ def test_env_defaults_js():
     assert r[1] == {"mode": "negacyclic", "device": 3}
     assert r[2] == {"mode": "compat", "device": 2}
     assert r[3] is True
+
+
+# ------------------------------------------------------------ measurement plumbing
+def test_build_id_and_bench_kernels_exist():
+    """fhe_build_id() is the Makefile's source hash, and every exact kernel
+    symbol bench.py attaches a profile to (BENCH_KERNELS) is in the build: a
+    renamed or re-templated kernel must update the table, never silently
+    match a stale profile."""
+    import glob
+    import sys
+
+    bid = fhe_gpu.build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid), bid
+    hdr = os.path.join(ROOT, "node-fhe-accelerate_amd", "build", "obj", "build_id.h")
+    if os.path.exists(hdr):
+        assert bid in open(hdr).read()
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as kr
+
+    if not glob.glob(os.path.join(kr.OBJ_DIR, "*.o")):
+        pytest.skip("objects not built (run __graft_entry__.build())")
+    names = set(kr.demangle([k["name"] for k in kr.kernels()]))
+    sys.path.insert(0, ROOT)
+    import bench
+
+    missing = {k: s for k, s in bench.BENCH_KERNELS.items() if s not in names}
+    assert not missing, missing

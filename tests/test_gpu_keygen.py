@@ -13,6 +13,8 @@ import oracle
 P27 = 132120577
 P62 = 4611686018326724609
 Q50 = 1125899906826241  # Q_50_1 (tfhe-128-balanced)
+Q63 = 9223370937344327681  # just below 2^63
+QG = 18446744069414584321  # 2^64 - 2^32 + 1: (int64_t)q < 0 in the reference's Gaussian loop
 SEED = [0x0123456789ABCDEF, 0x0F1E2D3C4B5A6978, 42, 7]
 
 
@@ -27,9 +29,11 @@ gpu = pytest.mark.gpu
 
 
 @gpu
-@pytest.mark.parametrize("q", [97, P27, Q50, P62])
+@pytest.mark.parametrize("q", [97, P27, Q50, P62, Q63, QG])
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
 def test_sample_vs_oracle(fg, q, kind):
+    """Every sampler vs the oracle; at QG the Gaussian's negative samples
+    take the closed form of the reference loop's int64 wrap (keygen.hip)."""
     ring = fg.PolynomialRing(16 if q == 97 else 1024, q)  # 97 = 3 * 2^5 + 1: degrees up to 16
     for count in (1, 1000, 65536 + 3):
         got = fg.sample(ring, kind, SEED, 11, count, std_dev=3.2)
@@ -56,7 +60,8 @@ def test_sample_device_output_and_statistics(fg):
 
 @gpu
 @pytest.mark.parametrize("n,q,mode", [(1024, P27, "compat"), (4096, P62, "compat"), (2048, Q50, "negacyclic"),
-                                      (8192, 1152921504606584833, "compat")])
+                                      (8192, 1152921504606584833, "compat"), (1024, Q63, "compat"),
+                                      (1024, QG, "compat")])
 def test_public_and_eval_key_vs_oracle(fg, n, q, mode):
     ring = fg.PolynomialRing(n, q, mode=mode)
     ref = oracle.NTT(n, q) if mode == "compat" else None

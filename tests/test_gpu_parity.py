@@ -238,6 +238,45 @@ def test_large_degree_chunk_boundaries(fg):
         assert torch.equal(x, m)
 
 
+@pytest.mark.parametrize("n,q", [(32768, P27), (65536, P62)])
+def test_large_degree_host_staging_chunks(fg, n, q, monkeypatch):
+    """Host arrays at N > 16384 with an 8 MiB staging buffer (FHE_STAGE_MB,
+    read per call): one call spans at least three staging chunks, each on
+    its own stream, all sharing the context's big-N scratch (ordered by
+    BigSync, fhe_internal.hpp).  Every row vs the oracle; a ciphertext
+    multiply (2 polys in, 3 out per unit) across the chunks as well."""
+    monkeypatch.setenv("FHE_STAGE_MB", "8")
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    per_chunk = (8 << 20) // (n * 8)
+    b = 3 * per_chunk + 3  # ragged last chunk
+    x = oracle.splitmix_fill(n + 41, q, b * n).reshape(b, n)
+    y = oracle.splitmix_fill(n + 42, q, b * n).reshape(b, n)
+    assert (r.forward_ntt(x) == t.forward(x)).all()
+    assert (r.multiply(x, y) == t.polymul(x, y)).all()
+    assert (r.forward_ntt_mul(x, y) == t.fwd_mul(x, y)).all()
+    eng = fg.EncryptionEngine(r)
+    nct = (8 << 20) // (3 * n * 8) * 3 + 1  # three chunks of whole ciphertexts and one more
+    cx = x[: 2 * nct].reshape(nct, 2, n)
+    cy = y[: 2 * nct].reshape(nct, 2, n)
+    got = eng.multiply(cx, cy)
+    for i in (0, nct // 2, nct - 1):
+        assert (got[i] == t.ct_multiply(cx[i], cy[i])).all(), i
+
+
+def test_large_degree_golden_ct_multiply(fg, golden_dir):
+    """EncryptionEngine::multiply at the two-pass degrees vs the committed
+    golden hash (two ciphertexts from the ntt_large seeds)."""
+    for c in load(golden_dir, "ntt_large.json"):
+        if "sha_ct_multiply" not in c:
+            continue
+        n, q = c["n"], c["q"]
+        r = fg.PolynomialRing(n, q)
+        x = oracle.splitmix_fill(c["seed_x"], q, 4 * n).reshape(2, 2, n)
+        y = oracle.splitmix_fill(c["seed_y"], q, 4 * n).reshape(2, 2, n)
+        assert _sha(fg.EncryptionEngine(r).multiply(x, y)) == c["sha_ct_multiply"], (n, q)
+
+
 @pytest.mark.parametrize("n,q,bl,lv,k", [(32768, P62, 23, 1, 1), (65536, P27, 9, 3, 1), (1024, P62, 15, 2, 2),
                                          (256, 7681, 4, 3, 3), (32768, P27, 10, 2, 2)])
 def test_external_product_composed_vs_oracle(fg, n, q, bl, lv, k):

@@ -137,3 +137,69 @@ def test_wide_fused_only_entry_points_report_unsupported(fg):
     with pytest.raises(fg.FHEError) as ei:
         fg.PublicKey(r, np.zeros((2, 1024), np.uint64))
     assert ei.value.code == -10 and "2^62" in str(ei.value)
+
+
+# ------------------------------------------------------------ q >= 2^63, negacyclic
+# Compat mode at q >= 2^63 reproduces the reference's zero inverse, so its
+# inverse-side paths compare zeros with zeros.  Negacyclic mode uses the true
+# inverses: these checks exercise the wide inverse (the HBM stage kernel at
+# N > 16384) and the 65-bit key MAC with non-zero data, through the identity
+# p(x) for a root x of X^N + 1 (x = psi^(2j+1)): ring products evaluate to
+# products, so every output is checked exactly at several such points.
+def _roots(q, psi, count=3):
+    return [pow(psi, 2 * j + 1, q) for j in (1, 1234, 98765)[:count]]
+
+
+def _ev(p, x, q):
+    acc = 0
+    for c in reversed([int(v) for v in np.asarray(p).ravel()]):
+        acc = (acc * x + c) % q
+    return acc
+
+
+@pytest.mark.parametrize("n", [32768, 65536])
+def test_wide_negacyclic_big_degree_qg(fg, n):
+    q = QG
+    r = fg.PolynomialRing(n, q, mode="negacyclic")
+    x = oracle.splitmix_fill(n + 3, q, 2 * n).reshape(2, n)
+    y = oracle.splitmix_fill(n + 4, q, 2 * n).reshape(2, n)
+    f = r.forward_ntt(x)
+    assert (r.inverse_ntt(f) == x).all()
+    m = r.multiply(x, y)
+    for pt in _roots(q, r.primitive_root):
+        for i in range(2):
+            assert _ev(m[i], pt, q) == _ev(x[i], pt, q) * _ev(y[i], pt, q) % q
+    # the forward transform is evaluation: X_k = a(psi^(2 brv-free k + 1)) for some ordering;
+    # inverse(pointwise(fwd x, fwd y)) is the same product
+    assert (r.inverse_ntt(r.pointwise_multiply(f, r.forward_ntt(y))) == m).all()
+
+
+@pytest.mark.parametrize("n", [1024, 32768])
+def test_wide_negacyclic_relinearize_and_extprod_qg(fg, n):
+    """relinearize (encryption.cpp:904-980): c_j' = c_j + sum_l d_l(c2) rlk_l
+    with unsigned digits d_l = (c2 >> l B) & (2^B - 1); external product
+    (bootstrap_engine.cpp:431-518): res_j = sum_r D_r g_rj with the signed
+    TFHE digits -- both checked by evaluation at roots of X^N + 1."""
+    q = QG
+    r = fg.PolynomialRing(n, q, mode="negacyclic")
+    eng = fg.EncryptionEngine(r)
+    bl, lv = 16, 4
+    ct3 = oracle.splitmix_fill(41, q, 3 * n).reshape(1, 3, n)
+    rlk = oracle.splitmix_fill(42, q, lv * 2 * n).reshape(lv, 2, n)
+    out = eng.relinearize(ct3, fg.EvaluationKey(r, rlk, bl))[0]
+    c2 = ct3[0, 2]
+    digits = [(c2 >> np.uint64(l * bl)) & np.uint64((1 << bl) - 1) for l in range(lv)]
+    for pt in _roots(q, r.primitive_root, 2):
+        d = [_ev(dl, pt, q) for dl in digits]
+        e0 = (_ev(ct3[0, 0], pt, q) + sum(d[l] * _ev(rlk[l, 1], pt, q) for l in range(lv))) % q
+        e1 = (_ev(ct3[0, 1], pt, q) + sum(d[l] * _ev(rlk[l, 0], pt, q) for l in range(lv))) % q
+        assert (_ev(out[0], pt, q), _ev(out[1], pt, q)) == (e0, e1)
+    k, bl, lv = 1, 20, 2
+    ggsw = oracle.splitmix_fill(43, q, (k + 1) * lv * (k + 1) * n).reshape((k + 1) * lv, k + 1, n)
+    glwe = oracle.splitmix_fill(44, q, (k + 1) * n).reshape(1, k + 1, n)
+    got = fg.ExternalProduct(r, ggsw, bl, lv, k)(glwe)[0]
+    rows = np.concatenate([oracle.decompose(q, glwe[0, i], bl, lv) for i in range(k + 1)])
+    for pt in _roots(q, r.primitive_root, 2):
+        dv = [_ev(rw, pt, q) for rw in rows]
+        for j in range(k + 1):
+            assert _ev(got[j], pt, q) == sum(dv[t] * _ev(ggsw[t, j], pt, q) for t in range(len(rows))) % q

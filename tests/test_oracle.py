@@ -331,3 +331,41 @@ def test_keygen_restatements_are_consistent():
     assert ka.shape == (16, 5) and kb.shape == (16,)
     v, ph = oracle.lwe_decrypt(q, 4, lwe, ka[0], kb[0])
     assert 0 <= ph < q and 0 <= v < 4
+
+
+def test_gaussian_wrap_closed_form_matches_loop():
+    """The reference's Gaussian at q >= 2^63 (key_manager.cpp:102-109):
+    (int64_t)q is negative, so the `while (v < 0) v += q` loop ends only when
+    the sum wraps past INT64_MIN.  ref_cpu.c / keygen.hip compute that wrapped
+    value in closed form (k = floor((v + 2^63) / m) + 1, m = 2^64 - q); here
+    the same derivation at 16-bit width is checked against the literal loop."""
+    import random
+
+    B = 16
+
+    def wrap(x):
+        x &= (1 << B) - 1
+        return x - (1 << B) if x >> (B - 1) else x
+
+    rnd = random.Random(5)
+    for _ in range(5000):
+        q = rnd.randrange((1 << (B - 1)) | 1, 1 << B, 2)
+        v = -rnd.randrange(1, 40)
+        s = wrap(wrap(q) + v)
+        while s < 0:
+            s = wrap(s + wrap(q))
+        m = (1 << B) - q
+        k = (v + (1 << (B - 1))) // m + 1
+        assert (s & ((1 << B) - 1)) % q == ((v - k * m) & ((1 << B) - 1)) % q
+
+
+def test_gaussian_wide_modulus_terminates():
+    """q = 2^64 - 2^32 + 1: the oracle returns at once, every value < q, and
+    the non-negative samples are the plain rounded draws."""
+    QG = 18446744069414584321
+    seed = [1, 2, 3, 4]
+    v = oracle.sample(2, seed, 9, QG, 4096, 3.2)
+    assert (v < np.uint64(QG)).all()
+    same = oracle.sample(2, seed, 9, 4611686018326724609, 4096, 3.2)
+    small = same < np.uint64(64)  # non-negative draws are the same at both moduli
+    assert small.sum() > 1000 and (v[small] == same[small]).all()

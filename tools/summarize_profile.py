@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarize a rocprofv3 run of tools/gpu_profile.sh into profiles/<tag>/.
+"""Summarize a rocprofv3 run of tools/gpu_evidence.sh into profiles/<tag>/.
 
 Per kernel of interest: average duration (kernel trace stats), and per
 launch the PMC counters.  HBM traffic per launch follows
@@ -11,7 +11,12 @@ Only launches of the full benchmark batch are used (the bench's 2-row parity
 spot check is excluded by grid size).
 
 usage: summarize_profile.py gpurun_out/prof_<tag> profiles/<tag> [--kernel-substr fwd_mul]
-       [--workload kernel,n,batch,q]
+       [--workload kernel,n,batch,q[,mode]] [--build-id ID]
+
+The summary records the exact demangled name of the profiled kernel (the
+full-batch launches matching the substring) and the build id of the library
+the run loaded (fhe_build_id()); bench.py uses a summary only when both match
+the kernel it launches and the library it runs.
 """
 import csv
 import glob
@@ -30,6 +35,8 @@ def main():
 
     out = {"source": src, "kernel_substr": ksub,
            "generated": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
+    if "--build-id" in sys.argv:
+        out["build_id"] = sys.argv[sys.argv.index("--build-id") + 1]
     if "--workload" in sys.argv:
         parts = sys.argv[sys.argv.index("--workload") + 1].split(",")
         k, n, b, q = parts[:4]
@@ -52,10 +59,10 @@ def main():
             out["kernel_stats_name"] = top["Name"][:160]
             out["kernel_avg_ns"] = float(top["AverageNs"])
     per_counter = defaultdict(list)
-    grid = {}
+    full_names = set()
     for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
         acc = defaultdict(float)
-        names = {}
+        names, grid, meta = {}, {}, {}
         for r in csv.DictReader(open(f)):
             if ksub not in r["Kernel_Name"]:
                 continue
@@ -63,15 +70,32 @@ def main():
             acc[key] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"]
             grid[r["Dispatch_Id"]] = int(r["Grid_Size"])
-            out["vgpr"] = r.get("VGPR_Count")
-            out["lds_bytes"] = r.get("LDS_Block_Size")
-            out["kernel_name"] = r["Kernel_Name"]
+            meta[r["Dispatch_Id"]] = (r.get("VGPR_Count"), r.get("LDS_Block_Size"))
         if not acc:
             continue
         gmax = max(grid.values())
+        for d, g in grid.items():
+            if g == gmax:
+                full_names.add(names[d])
+                out["vgpr"], out["lds_bytes"] = meta[d]
         for (d, c), v in acc.items():
             if grid[d] == gmax:
                 per_counter[c].append(v)
+    if len(full_names) == 1:
+        out["kernel_name"] = next(iter(full_names))
+        # per-dispatch durations of that exact kernel at the full grid, from
+        # the kernel trace (kernel_stats averages every launch of the name)
+        for tf in glob.glob(os.path.join(src, "trace", "*kernel_trace.csv")):
+            durs, gmax = [], 0
+            rows = [r for r in csv.DictReader(open(tf)) if r["Kernel_Name"] == out["kernel_name"]]
+            for r in rows:
+                gmax = max(gmax, int(r["Grid_Size_X"]))
+            durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if int(r["Grid_Size_X"]) == gmax]
+            if durs:
+                out["kernel_trace_full_batch"] = {"dispatches": len(durs), "avg_ns": sum(durs) / len(durs),
+                                                  "min_ns": min(durs), "max_ns": max(durs)}
+    elif full_names:  # several kernels match: ambiguous, bench.py will not use it
+        out["kernel_names"] = sorted(full_names)
     pmc = {c: sum(v) / len(v) for c, v in per_counter.items()}
     out["pmc_per_launch_avg"] = pmc
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
