@@ -87,8 +87,9 @@ int fhe_detect(fhe_hw_caps *caps);
  * Validation order and messages follow the reference constructor.  n must
  * be a power of two in [4, 65536]; the GPU kernels implement every such n
  * and every odd q whose root search succeeds: q < 2^62 in the lazy kernel
- * family, 2^62 <= q < 2^64 in the canonical one (ntt_wide.hip; there the
- * fused-only encrypt / decrypt / add_plain return FHE_ERR_UNSUPPORTED and
+ * family, 2^62 <= q < 2^64 in the canonical one (ntt_wide.hip; there
+ * encrypt / decrypt / add_plain are composed from batched transforms,
+ * engine_composed.hip, as they are for n > 16384, and
  * compat mode keeps the reference's psi^-1 and N^-1, which are not inverses
  * at q >= 2^63, ntt_processor.cpp:63-89).  n > 16384 runs as a
  * two-pass row/column split and the context holds 512 MiB of device
@@ -257,9 +258,12 @@ int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t
  * values per ciphertext encoded as (v * delta mod 2^64) mod q
  * (encode_packed :117-131; encode_plaintext is the one-slot case).
  * fhe_secret_key_prepare  sk [n] (SecretKey::poly) -> sk_prep [2][n]
- *   (NTT-domain s and s^2, Montgomery form; decrypt :256-271).
+ *   (NTT-domain s and s^2; decrypt :256-271).
  * fhe_public_key_prepare  pk [2][n] = (a, b) (PublicKey, key_manager.h:70-76)
- *   -> pk_prep [2][n] (NTT-domain, Montgomery form).
+ *   -> pk_prep [2][n] (NTT-domain).
+ *   Prepared keys are opaque to the caller: Montgomery form for the fused
+ *   kernels (q < 2^62, n <= 16384), canonical rows for the composed path
+ *   (q >= 2^62 or n > 16384); pass them back to the context that made them.
  * fhe_encrypt_batch  encrypt_internal (:171-205) with the sampled
  *   polynomials supplied (u ternary, e1, e2 error; [batch][n] each, any u64
  *   as x mod q), so the call is deterministic: ct [batch][2][n] =
@@ -275,7 +279,9 @@ int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t
  *   "Noise budget exhausted" failure.
  * fhe_add_plain_batch  add_plain (:638-665): out = (c0 + m, c1), m
  *   transformed first when is_ntt.
- * Degrees up to 16384 (add_plain on coefficient-form ciphertexts: any). */
+ * Every degree and modulus the context takes: one fused kernel per call for
+ * q < 2^62 and n <= 16384, batched transforms plus elementwise passes
+ * otherwise (engine_composed.hip). */
 int fhe_secret_key_prepare(fhe_ctx *ctx, const uint64_t *sk, uint64_t *sk_prep, int where);
 int fhe_public_key_prepare(fhe_ctx *ctx, const uint64_t *pk, uint64_t *pk_prep, int where);
 int fhe_encrypt_batch(fhe_ctx *ctx, uint64_t t, const uint64_t *pk_prep, const uint64_t *values, const uint64_t *u,

@@ -37,6 +37,7 @@ struct Plan {
     int word;   // 32 or 64
     int wide;   // q >= 2^62: every transform takes ntt_wide.hip
     int lazy;   // 32-bit path with (4 + 2L) q <= 2^32: forward stages skip reductions
+    int cus;    // compute units of the context's device (persistent grids)
     hipStream_t stream;
     // N > 2^kMaxFusedLogN (ntt_big.hip): two chunk-sized scratch buffers
     uint64_t *big_scratch[2];
@@ -106,6 +107,18 @@ hipError_t launch_decrypt(const Plan &p, uint64_t t, const uint64_t *sk_prep, co
                           int is_ntt, uint64_t *phase, int store_phase, uint64_t *dec, uint64_t *noise, size_t batch);
 hipError_t launch_add_plain(const Plan &p, uint64_t t, const uint64_t *ct, const uint64_t *vals, int is_ntt,
                             uint64_t *out, size_t batch);
+// Composed encrypt / decrypt / add_plain (engine_composed.hip) for q >= 2^62
+// and N > 16384: elementwise finishing passes around batched transforms.
+hipError_t launch_enc_finish(uint64_t q, uint64_t t, const uint64_t *t0, const uint64_t *t1, const uint64_t *e1,
+                             const uint64_t *e2, const uint64_t *vals, uint64_t *ct, uint32_t n, size_t batch,
+                             hipStream_t s);
+hipError_t launch_sub_row(uint64_t q, const uint64_t *src, uint32_t comps, const uint64_t *x, uint64_t *out, uint32_t n,
+                          size_t batch, hipStream_t s);
+hipError_t launch_decode(uint64_t q, uint64_t t, const uint64_t *phase, uint64_t *dec, uint64_t *noise, uint32_t n,
+                         size_t batch, hipStream_t s);
+hipError_t launch_add_plain_fin(uint64_t q, const uint64_t *ct, const uint64_t *f, uint64_t *out, uint32_t n, size_t batch,
+                                hipStream_t s);
+hipError_t launch_encode(uint64_t q, uint64_t t, const uint64_t *vals, uint64_t *out, size_t count, hipStream_t s);
 // acc [batch][k1][n] = (0, .., 0, test_poly): bootstrap's accumulator
 hipError_t launch_glwe_init(const uint64_t *test_poly, uint64_t *acc, uint32_t n, uint32_t k1, size_t batch,
                             hipStream_t s);

@@ -797,6 +797,10 @@ __device__ __forceinline__ void load_coeffs(W (&v)[E], uint64_t lim, uint64_t q,
 #ifndef FHE_LOAD_INFLIGHT
 #define FHE_LOAD_INFLIGHT 1
 #endif
+// coefficients per load chunk of the paired transforms (fwd_poly2)
+#ifndef FHE_POLY2_CH
+#define FHE_POLY2_CH 8
+#endif
 // As load_coeffs, for 32 coefficients per thread: raw u64 words are 2 VGPRs
 // each, so only IN chunks of CH are in flight at once and each chunk is
 // narrowed before the next is issued (scheduling barriers keep the compiler
@@ -895,13 +899,13 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     const uint32_t vo = tau * 8u;
     {
         const auto r = brsrc(src);
-        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
+        load_coeffs_chunked<G::E, FHE_POLY2_CH, FHE_LOAD_INFLIGHT>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
         });
     }
     {
         const auto r = brsrc(src2);
-        load_coeffs_chunked<G::E, 8, FHE_LOAD_INFLIGHT>(v2, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
+        load_coeffs_chunked<G::E, FHE_POLY2_CH, FHE_LOAD_INFLIGHT>(v2, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
             return bload(r, vo, cbrv(t, G::LOGE) * G::T * 8u);
         });
     }

@@ -52,6 +52,18 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 #ifndef FHE_FWDMUL_PREFETCH
 #define FHE_FWDMUL_PREFETCH 1
 #endif
+// 32 words per thread: w in chunks of FHE_FWDMUL_CH words, FHE_FWDMUL_PD
+// chunks in flight ahead of their use, the first FHE_FWDMUL_HOOK of them
+// issued inside the transform's last pass
+#ifndef FHE_FWDMUL_CH
+#define FHE_FWDMUL_CH 4
+#endif
+#ifndef FHE_FWDMUL_PD
+#define FHE_FWDMUL_PD 1
+#endif
+#ifndef FHE_FWDMUL_HOOK
+#define FHE_FWDMUL_HOOK 1
+#endif
 template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
 k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, uint64_t *__restrict__ out,
@@ -85,6 +97,46 @@ k_ntt_fwd_mul(const uint64_t *__restrict__ in, const uint64_t *__restrict__ wv, 
         const auto ro = brsrc(dst);
 #pragma unroll
         for (int e = 0; e < G::E; ++e) bstore(ro, vo, LastIO<LOGN>::so(e), (uint64_t)A.ar.red1q(A.ar.mont(v[e], w[e])));
+        return;
+    }
+#endif
+#if FHE_FWDMUL_PREFETCH
+    if constexpr (G::P == 1 && G::E == 32) {
+        // 32 words per thread (64-bit lanes): w streams in chunks of 8 --
+        // the first FHE_FWDMUL_PD chunks are issued in the last pass (hook),
+        // then chunk c + IN is issued before chunk c is consumed, so the
+        // loads of w overlap the transform's tail and each other instead of
+        // one round trip per chunk after the transform.
+        constexpr int CH = FHE_FWDMUL_CH, NC = G::E / CH;
+        uint64_t rw[G::E];
+        const uint32_t vo = LastIO<LOGN>::vo(tau);
+        const auto rwr = brsrc(wp);
+        auto issue = [&](int c) {
+#pragma unroll
+            for (int e = c * CH; e < c * CH + CH; ++e) rw[e] = bload(rwr, vo, LastIO<LOGN>::so(e));
+        };
+        auto hook = [&] {
+#pragma unroll
+            for (int c = 0; c < FHE_FWDMUL_HOOK && c < NC; ++c) issue(c);
+        };
+        fwd_poly<LOGN, LAZY, kPfSingle, true>(lds, v, tau, in + poly * G::N, valid, A, 0, hook);
+        const auto ro = brsrc(dst);
+#pragma unroll
+        for (int c = FHE_FWDMUL_HOOK; c < FHE_FWDMUL_PD && c < NC; ++c) issue(c);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c + FHE_FWDMUL_PD < NC) issue(c + FHE_FWDMUL_PD);
+            __builtin_amdgcn_sched_barrier(0);
+            W w[CH];
+            uint64_t r8[CH];
+#pragma unroll
+            for (int e = 0; e < CH; ++e) r8[e] = rw[c * CH + e];
+            coeffs_from_raw<CH>(w, r8, A.q64, SlowRed<W>{A});
+#pragma unroll
+            for (int e = 0; e < CH; ++e)
+                bstore(ro, vo, LastIO<LOGN>::so(c * CH + e), (uint64_t)A.ar.red1q(A.ar.mont(v[c * CH + e], w[e])));
+            __builtin_amdgcn_sched_barrier(0);
+        }
         return;
     }
 #endif

@@ -34,7 +34,12 @@ def rnd(seed, q, *shape):
     return oracle.splitmix_fill(seed, q, int(np.prod(shape))).reshape(shape)
 
 
-SIZES = [(16, 97), (256, 7681), (1024, P27), (1024, P62), (4096, P27), (8192, P62), (16384, P27), (16384, P62)]
+Q62 = 4611686018429485057     # 2^62 + 2^21 + 1
+Q63 = 9223370937344327681     # just below 2^63
+QG = 18446744069414584321     # 2^64 - 2^32 + 1
+SIZES = [(16, 97), (256, 7681), (1024, P27), (1024, P62), (4096, P27), (8192, P62), (16384, P27), (16384, P62),
+         # composed paths (engine_composed.hip): q >= 2^62 and N > 16384
+         (1024, Q62), (1024, Q63), (4096, QG), (32768, P27), (32768, P62), (65536, P27)]
 
 
 @pytest.mark.parametrize("n,q", SIZES)
@@ -79,7 +84,7 @@ def test_decrypt_vs_oracle(fg, n, q, comps):
         assert (res2.values == res.values).all() and (res2.max_noise == res.max_noise).all()
 
 
-@pytest.mark.parametrize("n,q", [(16, 97), (1024, P27), (4096, P62), (16384, P27)])
+@pytest.mark.parametrize("n,q", [(16, 97), (1024, P27), (4096, P62), (16384, P27), (1024, QG), (32768, P62)])
 def test_add_plain_vs_oracle(fg, n, q):
     b, t = 3, 4
     r = fg.PolynomialRing(n, q)
@@ -99,8 +104,10 @@ def test_add_plain_vs_oracle(fg, n, q):
     assert (got[1] == o.add_plain(t, ct[1], one, False)).all()
 
 
-@pytest.mark.parametrize("n,q,t", [(16384, P27, 4), (16384, P62, 1 << 20), (4096, P27, 256)])
-@pytest.mark.parametrize("mode", ["compat", "negacyclic"])
+@pytest.mark.parametrize("n,q,t,mode", [(n, q, t, m) for n, q, t in [(16384, P27, 4), (16384, P62, 1 << 20),
+                                                                     (4096, P27, 256), (65536, P62, 256)]
+                                         for m in ("compat", "negacyclic")]
+                         + [(4096, QG, 1 << 20, "negacyclic"), (32768, Q63, 16, "negacyclic")])
 def test_encrypt_decrypt_identity_full_degree(fg, n, q, t, mode):
     """Size-independent property: the transform product is commutative and
     associative in both modes, so with pk = (a, a s) and e1 = e2 = 0 the phase

@@ -1,8 +1,8 @@
 """Moduli 2^62 <= q < 2^64 (ntt_wide.hip): the reference takes any odd u64 q
 whose root search succeeds (ntt_processor.cpp:140-153; every product is a
-128-bit %), so the GPU path must too.  HIP vs the CPU oracle, bit-exact;
-ring ops, the composed ciphertext paths, and the fused-only entry points'
-FHE_ERR_UNSUPPORTED.
+128-bit %), so the GPU path must too.  HIP vs the CPU oracle, bit-exact:
+ring ops and the composed ciphertext paths (encrypt / decrypt / add_plain
+in tests/test_gpu_engine.py).
 
 At q >= 2^63 the reference's NTTProcessor::mod_inverse (ntt_processor.cpp:
 63-89) runs its signed Euclid on a negative int64 modulus and returns 0 for
@@ -130,13 +130,15 @@ def test_wide_external_product(fg, q):
         assert (got[i] == t.external_product(k, bl, lv, glwe[i], ggsw)).all(), i
 
 
-def test_wide_fused_only_entry_points_report_unsupported(fg):
-    """encrypt / decrypt / add_plain run only as fused kernels (lazy
-    arithmetic): at q >= 2^62 their preparation reports FHE_ERR_UNSUPPORTED."""
+def test_wide_keys_prepare(fg):
+    """encrypt / decrypt / add_plain at q >= 2^62 are composed from the wide
+    transforms (engine_composed.hip; checked against the oracle in
+    tests/test_gpu_engine.py): the key preparation no longer refuses them."""
     r = fg.PolynomialRing(1024, QG)
-    with pytest.raises(fg.FHEError) as ei:
-        fg.PublicKey(r, np.zeros((2, 1024), np.uint64))
-    assert ei.value.code == -10 and "2^62" in str(ei.value)
+    pk = fg.PublicKey(r, np.zeros((2, 1024), np.uint64))
+    assert pk.prep.shape == (2, 1024) and not pk.prep.any()
+    sk = fg.SecretKey(r, np.zeros(1024, np.uint64))
+    assert not sk.prep.any()
 
 
 # ------------------------------------------------------------ q >= 2^63, negacyclic
