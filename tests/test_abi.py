@@ -268,3 +268,33 @@ def test_build_id_and_bench_kernels_exist():
 
     missing = {k: s for k, s in bench.BENCH_KERNELS.items() if s not in names}
     assert not missing, missing
+
+
+def test_typescript_declarations_match_exports():
+    """index.d.ts (the typed surface a TS caller binds against): every
+    declared value is exported by lib/index.js, and every method of the
+    reference FHEEngine interface (fhe-engine.ts:33-78, restated there)
+    exists on FHEEngineImpl.  No tsc in this image, so the check is by name."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("node"):
+        pytest.skip("node not installed")
+    pkg = os.path.join(ROOT, "node-fhe-accelerate_amd")
+    addon = os.path.join(pkg, "build", "fhe_napi.node")
+    if not os.path.exists(addon):
+        pytest.skip("N-API addon not built")
+    dts = open(os.path.join(pkg, "index.d.ts")).read()
+    values = set(re.findall(r"^export (?:declare )?(?:function|class|const|enum) (\w+)", dts, re.M))
+    body = dts[dts.index("export interface FHEEngine {"):]
+    body = body[:body.index("\n}")]
+    methods = re.findall(r"^\s+(\w+)\(", body, re.M)
+    assert len(methods) == 44, len(methods)
+    code = ("const m=require(%r);const E=m.FHEEngineImpl.prototype;"
+            "console.log(JSON.stringify({keys:Object.keys(m),"
+            "methods:Object.getOwnPropertyNames(E)}))" % os.path.join(pkg, "lib", "index.js"))
+    out = json.loads(subprocess.run(["node", "-e", code], capture_output=True, text=True, check=True).stdout)
+    missing = sorted(v for v in values if v not in out["keys"])
+    assert not missing, missing
+    absent = sorted(m for m in methods if m not in out["methods"])
+    assert not absent, absent
