@@ -110,8 +110,15 @@ __device__ __forceinline__ uint64_t not64(uint64_t x) {
 // A wave-uniform constant the compiler may no longer relate to its source
 // (x + launder(-k) stays a v_lshl_add_u64 instead of being folded back into
 // a borrow-chain subtraction x - k).
+#ifndef FHE_LAUNDER_SGPR
+#define FHE_LAUNDER_SGPR 1
+#endif
 __device__ __forceinline__ uint64_t launder(uint64_t c) {
+#if FHE_LAUNDER_SGPR
     asm("" : "+s"(c));
+#else
+    asm("" : "+r"(c));
+#endif
     return c;
 }
 // x < 2k, k < 2^63: x - k if x >= k else x

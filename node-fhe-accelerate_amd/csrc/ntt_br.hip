@@ -37,18 +37,35 @@ struct BrArgs {
     int level, base_log;
 };
 
+// Halves of N / 16 threads from N = 4096 (16 coefficients each: the
+// 32-per-thread geometry would hold 128 VGPRs of key words per row), of 128
+// threads below.
 template <int LOGN>
-constexpr int br_key() { return gk(LOGN, LOGN - 7); }
+constexpr int br_key() { return LOGN >= 12 ? gk(LOGN, 4) : gk(LOGN, LOGN - 7); }
+template <int LOGN>
+constexpr int br_threads() { return 2 * Geo<br_key<LOGN>()>::T; }
+// The cross-half MAC terms share the exchange regions when the accumulators,
+// two exchange regions and a separate cross buffer exceed the LDS (N = 4096
+// with 64-bit words: 64 + 66 + 64 KiB): one more barrier per row.
+template <int LOGN, typename W>
+constexpr bool br_alias_x() {
+    using G = Geo<br_key<LOGN>()>;
+    return 2 * G::N * 8 + 2 * G::LW * (int)sizeof(W) + 2 * G::N * (int)sizeof(W) > 160 * 1024;
+}
 
 template <int LOGN, typename W>
-__global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
+__global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, NttArgs<W> A) {
     constexpr int K = br_key<LOGN>();
     using G = Geo<K>;
-    static_assert(G::P == 2 && G::THREADS == 256, "two 128-thread halves per workgroup");
+    constexpr int THREADS = br_threads<LOGN>();
+    constexpr bool ALIAS = br_alias_x<LOGN, W>();
+    static_assert(G::LW >= G::N, "cross terms fit an exchange region");
     constexpr int N = G::N;
     __shared__ uint64_t accs[2][N];   // raw accumulators (component j)
     __shared__ W xlds[2 * G::LW];     // NTT exchange, one region per half
-    __shared__ W xbuf[2][N];          // cross-half MAC terms
+    __shared__ W xsep[ALIAS ? 1 : 2 * N];
+    // cross-half MAC terms: own buffer, or half h's exchange region
+    auto xb = [&](uint32_t h) -> W * { return ALIAS ? xlds + h * G::LW : xsep + h * N; };
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t ct = blockIdx.x;
     const uint64_t q = A.q64, mu = A.mu64;
@@ -57,7 +74,7 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
     {
         // acc <- X^-round(b 2N/q) acc   (k_rotate's map)
         const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
-        for (uint32_t i = threadIdx.x; i < 2u * N; i += G::THREADS) {
+        for (uint32_t i = threadIdx.x; i < 2u * N; i += THREADS) {
             const uint32_t j = i / N, p = i % N;
             accs[j][p] = rotated_at(gacc + (size_t)j * N, p, r0, N, q, mu);
         }
@@ -103,18 +120,22 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
             });
             fwd_pass<K, 0, false>(v, t0, A.ar);
             fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
+            // the other half may still read its exchange region (last pass)
+            if constexpr (ALIAS) __syncthreads();
             // raw output (< 4q) times a canonical key: a valid Montgomery pair
+            W *const xo = xb(1 - pl);
 #pragma unroll
             for (int e = 0; e < G::E; ++e) {
                 const uint32_t gi = gidx<K, G::NP - 1>(tr, e);
                 const W own = A.ar.mont(v[e], (W)kv[0][e]);
-                xbuf[1 - pl][gi] = A.ar.mont(v[e], (W)kv[1][e]);
+                xo[gi] = A.ar.mont(v[e], (W)kv[1][e]);
                 oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
             }
             __syncthreads();
+            const W *const xi = xb(pl);
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) oacc[e] = A.ar.red2q(oacc[e] + xbuf[pl][gidx<K, G::NP - 1>(tr, e)]);
-            __syncthreads();  // xbuf and the exchange regions are reused
+            for (int e = 0; e < G::E; ++e) oacc[e] = A.ar.red2q(oacc[e] + xi[gidx<K, G::NP - 1>(tr, e)]);
+            __syncthreads();  // the cross terms and the exchange regions are reused
         }
         // component pl: inverse, then acc_pl = mod_add(inv, red_q(acc_pl))
         uint32_t ti = tau;
@@ -127,7 +148,7 @@ __global__ void __launch_bounds__(256) k_br_persist(BrArgs D, NttArgs<W> A) {
                                                       });
         __syncthreads();
     }
-    for (uint32_t i = threadIdx.x; i < 2u * N; i += G::THREADS) gacc[i] = accs[i / N][i % N];
+    for (uint32_t i = threadIdx.x; i < 2u * N; i += THREADS) gacc[i] = accs[i / N][i % N];
 }
 
 // GLWE dimension k >= 2 (K1 = k + 1 >= 3 accumulators): the same one-launch
@@ -271,12 +292,12 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
     for (uint32_t i = threadIdx.x; i < (uint32_t)(K1 * N); i += G::THREADS) gacc[i] = accs[i / N][i % N];
 }
 
-// k1 == 2: N = 512..2048; k1 == 3 (GLWE dimension 2): N = 512 / 1024 (and
+// k1 == 2: N = 512..4096; k1 == 3 (GLWE dimension 2): N = 512 / 1024 (and
 // 2048 with 32-bit words), where the K1 accumulators and both halves'
 // partial sums fit in LDS.
 bool br_persist_supported(const Plan &p, int k1) {
     if (p.wide) return false;
-    if (k1 == 2) return p.logn >= 9 && p.logn <= 11;
+    if (k1 == 2) return p.logn >= 9 && p.logn <= 12;
     if (k1 == 3) return p.logn >= 9 && (p.logn <= 10 || (p.logn == 11 && p.word == 32));
     return false;
 }
@@ -284,7 +305,10 @@ bool br_persist_supported(const Plan &p, int k1) {
 template <int LOGN, typename W>
 static hipError_t br_one(const Plan &p, int k1, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
     if (k1 == 2) {
-        hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+        hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(br_threads<LOGN>()), 0, p.stream, D,
+                           A);
+    } else if constexpr (LOGN > 11) {
+        return hipErrorInvalidValue;
     } else {
         constexpr int LP = br_k_logp<LOGN, W, 3>();
         if constexpr (br_k_lds_bytes<LOGN, W, 3, LP>() <= 160 * 1024)
@@ -300,6 +324,7 @@ static hipError_t br_dispatch(const Plan &p, int k1, const BrArgs &D, size_t bat
     case 9: return br_one<9, W>(p, k1, D, batch, A);
     case 10: return br_one<10, W>(p, k1, D, batch, A);
     case 11: return br_one<11, W>(p, k1, D, batch, A);
+    case 12: return br_one<12, W>(p, k1, D, batch, A);
     default: return hipErrorInvalidValue;
     }
 }
