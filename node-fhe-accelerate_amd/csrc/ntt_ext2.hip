@@ -41,6 +41,13 @@
 #ifndef FHE_EXTACC_MC
 #define FHE_EXTACC_MC 4
 #endif
+// key chunks in flight ahead of their use; issue the first ones in the last pass
+#ifndef FHE_EXTACC_PD
+#define FHE_EXTACC_PD 1
+#endif
+#ifndef FHE_EXTACC_HOOK
+#define FHE_EXTACC_HOOK 0
+#endif
 
 namespace FHE_NS {
 
@@ -108,23 +115,38 @@ __global__ void __launch_bounds__(Geo<K>::THREADS, 2) k_extprod_acc(ExtAccArgs D
             stream_begin<K, 0, false, false>(tr, A.twf, t0);
             fwd_pass_stream<K, 0, false, false>(tr, v, t0, A.twf, A.ar);
         }
-        fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
-        // raw outputs (< 4q) times canonical prepared keys: valid Montgomery pairs
+        // The row's key words stream in chunks of MC coefficients: the first
+        // PD chunks are issued inside the transform's last pass (hook), then
+        // chunk c + PD before chunk c is consumed -- the L2 round trips
+        // overlap instead of following each other (they did, one per chunk).
         const auto rk = brsrc(D.key + (size_t)r * 2 * N);
-        const uint32_t vo = LastIO<K>::vo(tr);
+        constexpr int NC = E / MC, PD = FHE_EXTACC_PD;
+        uint64_t k0[E], k1[E];
+        auto issue = [&](int c) {
+            const uint32_t vo = LastIO<K>::vo(lane_index());
 #pragma unroll
-        for (int e0 = 0; e0 < E; e0 += MC) {
-            uint64_t k0[MC], k1[MC];
-#pragma unroll
-            for (int e = 0; e < MC; ++e) {
-                k0[e] = bload<0>(rk, vo, LastIO<K>::so(e0 + e));
-                k1[e] = bload<0>(rk, vo, LastIO<K>::so(e0 + e) + N * 8u);
+            for (int e = c * MC; e < c * MC + MC; ++e) {
+                k0[e] = bload<0>(rk, vo, LastIO<K>::so(e));
+                k1[e] = bload<0>(rk, vo, LastIO<K>::so(e) + N * 8u);
             }
+        };
+        auto hook = [&] {
 #pragma unroll
-            for (int e = 0; e < MC; ++e) {
-                const W m0 = A.ar.mont(v[e0 + e], (W)k0[e]), m1 = A.ar.mont(v[e0 + e], (W)k1[e]);
-                o0[e0 + e] = A.ar.red2q(o0[e0 + e] + m0);
-                o1[e0 + e] = A.ar.red2q(o1[e0 + e] + m1);
+            for (int c = 0; c < (FHE_EXTACC_HOOK ? PD : 0) && c < NC; ++c) issue(c);
+        };
+        fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar, hook);
+#pragma unroll
+        for (int c = FHE_EXTACC_HOOK ? PD : 0; c < PD && c < NC; ++c) issue(c);
+        // raw outputs (< 4q) times canonical prepared keys: valid Montgomery pairs
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c + PD < NC) issue(c + PD);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int e = c * MC; e < c * MC + MC; ++e) {
+                const W m0 = A.ar.mont(v[e], (W)k0[e]), m1 = A.ar.mont(v[e], (W)k1[e]);
+                o0[e] = A.ar.red2q(o0[e] + m0);
+                o1[e] = A.ar.red2q(o1[e] + m1);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
