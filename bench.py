@@ -639,7 +639,14 @@ def cpu_baseline(n, q, seconds, threads=None):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": done / el, "unit": "NTTs/s", "cores": threads, "kind": "port",
+    if threads == 1:
+        basis = "one thread (the reference's sequential forward_ntt_batch, ntt_processor.cpp:394-408)"
+    elif threads < info["affinity_cpus"]:
+        basis = ("the job's CPU share on this host (OMP_NUM_THREADS; the GPU box's affinity mask lists the whole "
+                 "shared machine, nproc above)")
+    else:
+        basis = "every CPU this process may run on"
+    return {"value": done / el, "unit": "NTTs/s", "cores": threads, "cores_basis": basis, "kind": "port",
             "calibration": "uncalibrated port: the reference C++ is not buildable here (modular_arithmetic.h "
                            "includes <arm_neon.h>), so the +-10% calibration of BASELINE.md section 2 was not possible",
             **info,
