@@ -85,8 +85,24 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
     W breg[AREG ? G::E : 1];
     // HBM slots (NL < 3) hold W words in the first half of their u64 row
     auto hrow = [&](int s) -> W * { return reinterpret_cast<W *>(orow + (size_t)(s + 1) * G::N); };
+    // FHE_DEBUG_SLOTS (debug build, tests/test_gpu_cipher.py run once with
+    // it): every slot access checks its slot number, register index and
+    // position -- the round-2 fault in this kernel had no identified cause,
+    // this is the guard that would name a bad index instead of faulting
+#ifndef FHE_DEBUG_SLOTS
+#define FHE_DEBUG_SLOTS 0
+#endif
+    auto check = [&](int s, uint32_t gi, int e) {
+        if constexpr (FHE_DEBUG_SLOTS) {
+            if (s < 0 || s > 2 || e < 0 || e >= G::E || gi >= (uint32_t)G::N) {
+                printf("k_ct_mul slot index out of range: s=%d e=%d gi=%u (E=%d N=%d)\n", s, e, gi, G::E, G::N);
+                __builtin_trap();
+            }
+        }
+    };
     // slot s at global index gi (own positions only)
     auto ld = [&](int s, uint32_t gi, int e) -> W {
+        check(s, gi, e);
         if (AREG && s == 0) return areg[AREG ? e : 0];
         if (AREG && s == 1) return breg[AREG ? e : 0];
         if (NL == 3 || (NL == 1 && s == 2)) return lds_all[G::P * G::LW + ((NL == 3 ? s : 0) * G::P + pl) * G::N + gi];
@@ -94,6 +110,7 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
         return valid ? hrow(s)[gi] : W(0);
     };
     auto st = [&](int s, uint32_t gi, int e, W val) {
+        check(s, gi, e);
         if (AREG && s == 0) areg[AREG ? e : 0] = val;
         else if (AREG && s == 1) breg[AREG ? e : 0] = val;
         else if (NL == 3 || (NL == 1 && s == 2)) lds_all[G::P * G::LW + ((NL == 3 ? s : 0) * G::P + pl) * G::N + gi] = val;
@@ -126,6 +143,7 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
         }
     };
     auto slot = [&](int s, int k, uint32_t gi, int e) -> W {
+        check(s, gi, e);
         if (AREG && s == 0) return areg[AREG ? e : 0];
         if (AREG && s == 1) return breg[AREG ? e : 0];
         if constexpr (HB) return pre[k][e];

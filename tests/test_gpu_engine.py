@@ -141,7 +141,7 @@ def test_encrypt_decrypt_identity_full_degree(fg, n, q, t, mode):
     assert (res.phase.cpu().numpy().view(np.uint64) == oracle.encode(q, t, m)).all()
     if mode == "negacyclic":
         e = rnd(905, 7, 2, b, n).astype(np.int64) - 3
-        e = np.where(e < 0, e + q, e).astype(np.uint64)
+        e = np.where(e < 0, np.uint64(q) - (-e).astype(np.uint64), e.astype(np.uint64)).astype(np.uint64)
         ct = eng.encrypt(D(m), pk, D(u), D(e[0]), D(e[1]))
         res = eng.decrypt(ct, key)
         assert (res.values.cpu().numpy().view(np.uint64) == m).all() and res.success.all()
