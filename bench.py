@@ -534,7 +534,7 @@ BENCH_KERNELS = {
     "extprod_B23_L1": "void fhe::k_extprod2<14, unsigned long>(fhe::DmArgs, fhe::NttArgs<unsigned long>)",
     "extprod_B15_L2": "void fhe::k_extprod_acc<1294>(fhe::ExtAccArgs, fhe::NttArgs<unsigned long>)",
     "ct_multiply": "void fhe::k_ct_mul2<1294, unsigned int, true>" + _nargs("int"),
-    "relinearize": "void fhe::k_relin32<1294, true>(fhe::DmArgs, fhe::NttArgs<unsigned int>)",
+    "relinearize": "void fhe::k_dmac<14, unsigned int, 2, false, 1>(fhe::DmArgs, fhe::NttArgs<unsigned int>)",
 }
 
 

@@ -40,8 +40,13 @@ struct BrArgs {
 // Halves of N / 16 threads from N = 4096 (16 coefficients each: the
 // 32-per-thread geometry would hold 128 VGPRs of key words per row), of 128
 // threads below.
+#ifndef FHE_BR_LOGE
+#define FHE_BR_LOGE 4
+#endif
 template <int LOGN>
-constexpr int br_key() { return LOGN >= 12 ? gk(LOGN, 4) : gk(LOGN, LOGN - 7); }
+constexpr int br_key() {
+    return LOGN >= 12 ? gk(LOGN, FHE_BR_LOGE) : gk(LOGN, LOGN - 7 < FHE_BR_LOGE ? LOGN - 7 : FHE_BR_LOGE);
+}
 template <int LOGN>
 constexpr int br_threads() { return 2 * Geo<br_key<LOGN>()>::T; }
 // The cross-half MAC terms share the exchange regions when the accumulators,

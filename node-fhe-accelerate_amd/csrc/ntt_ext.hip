@@ -294,117 +294,12 @@ k_extprod2(DmArgs D, NttArgs<W> A) {
     inv_poly2<LOGN, PF>(lds, v0, v1, ti, orow, orow + G::N, A, A.ninv);
 }
 
-// Relinearisation at N = 16384 with 32-bit lanes (q < 2^30): 32 coefficients
-// per thread (radix-32 passes: 2 LDS exchanges per transform instead of 3),
-// 512 threads, one workgroup per CU at up to 256 VGPRs:
-//   * the lane's 32 c2 words stay in VGPRs (c2 is read once; digit l is
-//     (c2 >> l B) & (2^B - 1), LSB first, encryption.cpp:944-950); taken
-//     when L B <= 32, so only the low dword of each word is needed (other
-//     decompositions take k_dmac MODE 1);
-//   * NTT-domain accumulator 0 (c0' <- b_l) lives in LDS at the lane's own
-//     positions, accumulator 1 (c1' <- a_l) in VGPRs;
-//   * the key words of level l + 1 (b and a rows, canonical < q < 2^32: one
-//     dword each) are loaded while level l's digits are transformed, so no
-//     L2 round trip is exposed between levels (k_dmac MODE 1 read them in 8
-//     dependent rounds per level after each transform).
-// Same arithmetic as k_dmac MODE 1: digits through the lazy forward, the
-// Montgomery MAC with the NTT x R keys, canonical inverses, + c_j (mod_add).
-#ifndef FHE_RELIN32
-#define FHE_RELIN32 1
-#endif
-#ifndef FHE_RELIN32_PF
-#define FHE_RELIN32_PF 1
-#endif
-template <int K, bool LAZY>
-__global__ void __launch_bounds__(Geo<K>::THREADS, Geo<K>::THREADS / 256)
-k_relin32(DmArgs D, NttArgs<uint32_t> A) {
-    using W = uint32_t;
-    using G = Geo<K>;
-    static_assert(G::P == 1 && G::LOGE == 5, "one ciphertext per workgroup, 32 coefficients per thread");
-    __shared__ W lds[G::LW];
-    __shared__ W acc0[G::N];
-    const TidSource tid;
-    const size_t ct = blockIdx.x;
-    if (ct >= D.batch) return;
-    const uint64_t *srow = D.src + ct * 3 * G::N;
-    uint64_t *orow = D.out + ct * 2 * G::N;
-    // level * base_log <= 32 (launch_relin): every digit comes from the low
-    // 32 bits of its c2 word, so one dword per word is kept
-    uint32_t craw[G::E];
-    {
-        const uint32_t tau = tid();
-        const auto r = brsrc(srow + 2 * G::N);
-#pragma unroll
-        for (int t = 0; t < G::E; ++t)
-            craw[t] = __builtin_amdgcn_raw_buffer_load_b32(r, tau * 8u, cbrv(t, G::LOGE) * G::T * 8u, kAuxNT);
-    }
-    // key dwords of one level at the lane's last-pass positions
-    uint32_t kb[G::E], ka[G::E];
-    auto load_keys = [&](int l) {
-        const uint32_t tau = tid();
-        const auto rb = brsrc(D.key + ((size_t)2 * l + 1) * G::N), ra = brsrc(D.key + (size_t)2 * l * G::N);
-        const uint32_t vo = LastIO<K>::vo(tau);
-#pragma unroll
-        for (int e = 0; e < G::E; ++e) {
-            kb[e] = __builtin_amdgcn_raw_buffer_load_b32(rb, vo, LastIO<K>::so(e), 0);
-            ka[e] = __builtin_amdgcn_raw_buffer_load_b32(ra, vo, LastIO<K>::so(e), 0);
-        }
-    };
-    W racc[G::E];
-    const uint64_t mask = (1ull << D.base_log) - 1, lim = (uint64_t)A.ar.q2 * 2;
-    load_keys(0);
-    for (int l = 0; l < D.level; ++l) {
-        if (l > 0) __syncthreads();  // the previous transform's last exchange reads precede this one's stores
-        const uint32_t shift = uint32_t(l) * uint32_t(D.base_log);
-        const uint32_t tau = tid();
-        Tw<W> t0[PassTw<K, 0>::COUNT];
-        load_tw<K, 0>(tau, A.twf, t0);
-        // digit l of each c2 word (narrowed at once; a digit >= 4q -- only
-        // for 2^B > 4q -- takes the exact reduction)
-        W v[G::E];
-        uint32_t bad = 0;
-#pragma unroll
-        for (int t = 0; t < G::E; ++t) {
-            const uint64_t d = (uint64_t)(craw[t] >> shift) & mask;
-            bad |= uint32_t(d >= lim);
-            v[t] = W(d);
-        }
-        if (__builtin_expect(bad != 0, 0)) {
-#pragma unroll
-            for (int t = 0; t < G::E; ++t) {
-                const uint64_t d = (uint64_t)(craw[t] >> shift) & mask;
-                if (d >= lim) v[t] = W(mod64_slow(d, A.q64, A.mu64));
-            }
-        }
-        fwd_pass<K, 0, LAZY, W>(v, t0, A.ar);
-        fwd_rest<K, 1, LAZY, FHE_RELIN32_PF>(lds, v, tau, A.twf, A.ar);
-        const uint32_t tm = tid();
-        // raw forward output (< R) times canonical keys: valid Montgomery pairs
-#pragma unroll
-        for (int e = 0; e < G::E; ++e) {
-            const uint32_t gi = gidx<K, G::NP - 1>(tm, e);
-            const W m0 = A.ar.mont(v[e], kb[e]), m1 = A.ar.mont(v[e], ka[e]);
-            acc0[gi] = l == 0 ? m0 : A.ar.red2q(acc0[gi] + m0);
-            racc[e] = l == 0 ? m1 : A.ar.red2q(racc[e] + m1);
-        }
-        if (l + 1 < D.level) load_keys(l + 1);  // in flight across the next level's transform
-    }
-    // c_j' = c_j + inv(acc_j)   (mod_add of encryption.cpp:953 / 958)
-    const uint64_t q = A.q64, mu = A.mu64;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        __syncthreads();
-        const uint32_t tau = tid();
-        W v[G::E];
-#pragma unroll
-        for (int e = 0; e < G::E; ++e) v[e] = j == 0 ? acc0[gidx<K, G::NP - 1>(tau, e)] : racc[e];
-        const uint64_t *addend = srow + (size_t)j * G::N;
-        inv_poly_from_regs<K, FHE_RELIN32_PF>(lds, v, tau, orow + (size_t)j * G::N, true, A, A.ninv, 0,
-                                             [&](uint32_t gi, uint64_t x) -> uint64_t {
-                                                 return addq(x, red_q(addend[gi], q, mu), q);
-                                             });
-    }
-}
+// Relinearisation takes k_dmac MODE 1.  A 32-coefficient-per-thread kernel
+// (c2 low dwords and accumulator 1 in VGPRs, accumulator 0 in LDS, the next
+// level's keys in flight across each transform; 232 VGPRs, 8 waves per CU)
+// measured slower on MI355X: 9.03 vs 8.29 ms per 16,384 ciphertexts at
+// (L, B) = (7, 4) (round-4 A/B) -- the 16 waves of MODE 1 hide more of the
+// exchange barriers than the shorter transforms save.
 
 // FHE_EXT_ACC=0: multi-level external products at N = 16384 take k_dmac
 // (lab A/B against ntt_ext2.hip).
@@ -457,16 +352,6 @@ hipError_t launch_extprod(const Plan &p, int k1, int level, int base_log, const 
 hipError_t launch_relin(const Plan &p, int level, int base_log, const uint64_t *ct3, const uint64_t *rlk,
                         uint64_t *out, size_t batch) {
     DmArgs D{ct3, rlk, out, batch, level, base_log, nullptr, 0, 0, 0, nullptr};
-    if (FHE_RELIN32 && p.word == 32 && p.logn == 14 && level > 0 && batch > 0 && level * base_log <= 32) {
-        constexpr int K = gk(14, 5);
-        if (p.lazy)
-            hipLaunchKernelGGL((k_relin32<K, true>), dim3((unsigned)batch), dim3(Geo<K>::THREADS), 0, p.stream, D,
-                               p.a32);
-        else
-            hipLaunchKernelGGL((k_relin32<K, false>), dim3((unsigned)batch), dim3(Geo<K>::THREADS), 0, p.stream, D,
-                               p.a32);
-        return hipGetLastError();
-    }
     return dmac<1>(p, 2, D);
 }
 

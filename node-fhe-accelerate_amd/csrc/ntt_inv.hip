@@ -95,16 +95,9 @@ constexpr int polymul_occ() {
 #endif
 template <int LOGN, typename W>
 constexpr int inv_key() { return (FHE_INV64_E32 && sizeof(W) == 8 && LOGN == 14) ? gk(LOGN, 5) : LOGN; }
-// FHE_POLY_E16DUAL (lab): q < 2^30 at N = 16384 as the paired kernel at 16
-// coefficients per thread (1024 threads, <= 64 VGPRs: two workgroups and 8
-// waves per SIMD per CU).
-#ifndef FHE_POLY_E16DUAL
-#define FHE_POLY_E16DUAL 0
-#endif
 template <int LOGN, typename W>
 constexpr int polymul_key() {
     if (sizeof(W) == 8) return (FHE_POLY64 == 2 && LOGN == 14) ? gk(LOGN, 5) : LOGN;
-    if (FHE_POLY_E16DUAL && LOGN == 14) return gk(LOGN, 4);
     return (!FHE_POLY_E16 && sizeof(W) == 4 && LOGN >= 13 && LOGN <= 14) ? gk(LOGN, 5) : LOGN;
 }
 template <int LOGN>
@@ -124,7 +117,7 @@ template <int LOGN, typename W>
 constexpr bool polymul_dual() {
     using G = Geo<LOGN>;
     if constexpr (sizeof(W) == 4)
-        return (G::LOGE == 5 || (FHE_POLY_E16DUAL && G::L == 14 && G::LOGE == 4 && G::P == 1)) && FHE_POLY_DUAL;
+        return G::LOGE == 5 && FHE_POLY_DUAL;
     else return FHE_POLY_DUAL64 && G::P == 1 && G::L == 14 && G::LOGE == 4 && FHE_POLY64 == 1;
 }
 template <int LOGN, typename W>
@@ -198,59 +191,23 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
 // then the pointwise Montgomery product and the inverse.  Two workgroups per
 // CU (one 64 KiB exchange buffer each), so one's HBM traffic overlaps the
 // other's transforms.
-// Lab flags (measured A/B, profiles/r4*):
-//   FHE_POLY_PERSIST  > 0: a persistent grid of that many workgroups per CU,
-//                     each looping over pairs (0: one workgroup per pair);
-//   FHE_POLY_STAGGER  s_sleep(127) rounds before the first pair in the second
-//                     half of a persistent grid (phase offset between the two
-//                     workgroups of a CU);
-//   FHE_POLY_TOUCH    1: each workgroup first touches (plain loads, L2 /
-//                     Infinity Cache) the a, b lines of the pair one grid
-//                     ahead, consumed only at the end of its own pair.
-#ifndef FHE_POLY_PERSIST
-#define FHE_POLY_PERSIST 0
-#endif
-#ifndef FHE_POLY_STAGGER
-#define FHE_POLY_STAGGER 0
-#endif
-#ifndef FHE_POLY_TOUCH
-#define FHE_POLY_TOUCH 0
-#endif
+// A persistent grid (workgroups looping over pairs, with or without a phase
+// stagger or an L2 touch of the next pair) measured no faster (round 4).
 // lab only: 1 = HBM traffic without transforms, 2 = transforms without HBM
 #ifndef FHE_POLY_LAB
 #define FHE_POLY_LAB 0
 #endif
 template <int LOGN, typename W, bool LAZY>
 __device__ __forceinline__ void polymul2_one(W *lds, uint32_t tau, const uint64_t *__restrict__ a,
-                                             const uint64_t *__restrict__ b, uint64_t *c, size_t poly, size_t ahead,
-                                             size_t batch, const NttArgs<W> &A) {
+                                             const uint64_t *__restrict__ b, uint64_t *c, size_t poly,
+                                             const NttArgs<W> &A) {
     using G = Geo<LOGN>;
-    uint32_t touch[FHE_POLY_TOUCH ? 2 * (G::N / 16) / G::THREADS : 1];
-    if constexpr (FHE_POLY_TOUCH) {
-        // one 4-byte load per 128-byte line of the next pair's a and b
-        constexpr int PER = (G::N / 16) / G::THREADS;  // lines per thread per polynomial
-        if (ahead < batch) {
-            const uint32_t *ta = reinterpret_cast<const uint32_t *>(a + ahead * G::N);
-            const uint32_t *tb = reinterpret_cast<const uint32_t *>(b + ahead * G::N);
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                touch[i] = ta[(tau + i * G::THREADS) * 32];
-                touch[PER + i] = tb[(tau + i * G::THREADS) * 32];
-            }
-        }
-    }
     W v[G::E], vb[G::E];
     fwd_poly2<LOGN, LAZY, polymul2_pf<LOGN, W>()>(lds, v, vb, tau, a + poly * G::N, b + poly * G::N, A);
 #pragma unroll
     for (int e = 0; e < G::E; ++e) v[e] = A.ar.mont(fwd_to_canon<LAZY>(v[e], A), vb[e]);  // canonical x raw (< R)
     __syncthreads();  // the exchange buffer still holds b's last layout reads
     inv_poly_from_regs<LOGN, polymul2_pf<LOGN, W>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r);
-    if constexpr (FHE_POLY_TOUCH) {
-        if (ahead < batch) {
-#pragma unroll
-            for (int i = 0; i < (int)(sizeof(touch) / 4); ++i) asm volatile("" ::"v"(touch[i]));
-        }
-    }
 }
 
 template <int LOGN, typename W, bool LAZY>
@@ -261,14 +218,6 @@ k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint6
     static_assert(G::P == 1, "one polynomial pair per workgroup");
     __shared__ W lds[lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x;
-#if FHE_POLY_PERSIST
-    if (FHE_POLY_STAGGER && blockIdx.x >= gridDim.x / 2)
-        for (int i = 0; i < FHE_POLY_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-    for (size_t poly = blockIdx.x; poly < batch; poly += gridDim.x) {
-        polymul2_one<LOGN, W, LAZY>(lds, tau, a, b, c, poly, poly + gridDim.x, batch, A);
-        __syncthreads();  // the next pair's first exchange reuses the buffer
-    }
-#else
     const size_t poly = blockIdx.x;
     if (poly >= batch) return;
 #if FHE_POLY_LAB == 1
@@ -309,8 +258,7 @@ k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint6
         return;
     }
 #endif
-    polymul2_one<LOGN, W, LAZY>(lds, tau, a, b, c, poly, poly + 512, batch, A);
-#endif
+    polymul2_one<LOGN, W, LAZY>(lds, tau, a, b, c, poly, A);
 }
 
 template <int LOGN, typename W>
@@ -322,8 +270,6 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
     using GP = Geo<PK>;
     size_t pblocks = (batch + GP::P - 1) / GP::P;
     if constexpr (polymul_dual<PK, W>()) {
-        if (FHE_POLY_PERSIST && sizeof(W) == 4 && GP::LOGE == 5)
-            pblocks = std::min(pblocks, (size_t)FHE_POLY_PERSIST * (size_t)p.cus);
         if (b) {
             if constexpr (sizeof(W) == 4) {
                 if (lazy) {

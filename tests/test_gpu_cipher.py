@@ -80,8 +80,7 @@ def test_ct_multiply_negacyclic_is_ring_tensor(fg):
 @pytest.mark.parametrize("n,q,bl,lv", [(64, 257, 2, 4), (1024, P27, 4, 7), (1024, P27, 9, 3), (4096, P62, 16, 4),
                                        (8192, P62, 12, 5), (16384, P27, 4, 7), (16384, P62, 20, 3),
                                        (256, 7681, 63, 1),
-                                       # k_relin32 (L B <= 32) with the lazy and the non-lazy forward,
-                                       # and L B > 32 at N = 16384 (k_dmac MODE 1)
+                                       # L B <= 32 with a lazy and a non-lazy context, L B > 32, N = 16384
                                        (16384, P27, 8, 4), (16384, 1073643521, 4, 7), (16384, P27, 11, 3)])
 def test_relinearize_vs_oracle(fg, n, q, bl, lv):
     b = 2 if n >= 16384 else 4

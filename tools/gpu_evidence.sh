@@ -32,7 +32,7 @@ spec() {
     nega_fwd_mul) echo "--only fwd_mul --no-check --no-q62 --mode negacyclic|k_ntt_fwd_mul=fwd_mul,16384,65536,$P27,negacyclic";;
     nega_polymul) echo "--only polymul --no-check --no-q62 --mode negacyclic|k_polymul=polymul,16384,65536,$P27,negacyclic";;
     ct_mul)       echo "--only ct_mul|k_ct_mul=ct_mul,16384,8192,$P27";;
-    relin)        echo "--only relin|k_relin32=relin,16384,8192,$P27";;
+    relin)        echo "--only relin|k_dmac=relin,16384,8192,$P27";;
     c5)           echo "--only c5|k_extprod2=extprod_B23_L1,16384,4096,$P62 k_extprod_acc=extprod_B15_L2,16384,4096,$P62";;
     *) return 1;;
   esac
