@@ -22,6 +22,11 @@
 // Same arithmetic as MODE 2 (digit load, red_q / subq / addq, Montgomery MAC,
 // canonical inverse), so results are bit-identical to the multi-launch path
 // and to the oracle.
+// flag-free 64-bit arithmetic (fhe_arith.hpp): 19.0 vs 20.5 ms for the
+// N = 2048 preset, 94.9 vs 100.9 ms for the N = 1024 batch (round 4)
+#ifndef FHE_U64_NOVCC
+#define FHE_U64_NOVCC 1
+#endif
 #include "fhe_internal.hpp"
 #include "lwe_ops.hpp"
 
@@ -37,11 +42,15 @@ struct BrArgs {
     int level, base_log;
 };
 
-// Halves of N / 16 threads from N = 4096 (16 coefficients each: the
-// 32-per-thread geometry would hold 128 VGPRs of key words per row), of 128
-// threads below.
+// 8 coefficients per thread (N / 8 threads per half) from N = 1024, fewer
+// below: the transforms are throughput-bound on the one CU, and 16 per thread
+// (half the waves) measured 31.2 vs 20.7 ms (N = 2048, L = 2) and 70.7 vs
+// 58.6 ms (N = 4096, L = 3) per batch-64 blind rotation (round 4).
 #ifndef FHE_BR_LOGE
-#define FHE_BR_LOGE 4
+#define FHE_BR_LOGE 3
+#endif
+#ifndef FHE_BR_XACC
+#define FHE_BR_XACC 1
 #endif
 template <int LOGN>
 constexpr int br_key() {
@@ -64,6 +73,12 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
     using G = Geo<K>;
     constexpr int THREADS = br_threads<LOGN>();
     constexpr bool ALIAS = br_alias_x<LOGN, W>();
+    // the per-step difference held in VGPRs (2 E of them): spills beside
+    // 16-word spectra and at 1024 threads (128 VGPRs)
+    constexpr bool CV = G::E <= 8 && THREADS <= 512;
+    // the other half's MAC terms summed over the levels in VGPRs and
+    // exchanged once per step (else once per level through LDS)
+    constexpr bool XACC = FHE_BR_XACC && G::E <= 8 && (THREADS <= 512 || FHE_BR_XACC == 2);
     static_assert(G::LW >= G::N, "cross terms fit an exchange region");
     constexpr int N = G::N;
     __shared__ uint64_t accs[2][N];   // raw accumulators (component j)
@@ -87,14 +102,40 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
     __syncthreads();
     const int level = D.level;
     const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    // a negative digit's q - (base - d) is already below q
+    const bool small_base = base <= q;
     const size_t ggsw_words = (size_t)2 * level * 2 * N;
     const uint64_t *lwe_a = D.lwe_a + ct * D.lwe_dim;
+    bool canon = false;
     for (uint32_t step = 0; step < D.lwe_dim; ++step) {
         const int32_t r = rot_amount(lwe_a[step], N, D.lwe_q);  // workgroup-uniform
         if (r == 0) continue;
         const uint32_t rot = rot_norm(r, N);
         const uint64_t *key = D.bsk + ggsw_words * step;
-        W oacc[G::E];
+        W oacc[G::E], xacc[XACC ? G::E : 1];
+        // X^rot acc_pl - acc_pl at the lane's pass-0 positions: once per step
+        // into VGPRs where they fit (every level's digits come from it),
+        // else again for each level from the LDS accumulator.  After the
+        // first executed step every accumulator word is canonical (the
+        // mod_add below), and red_q / the wrap of (q - x) % q are the identity
+        // on it: the reductions are skipped (workgroup-uniform).
+        const uint64_t *ac = accs[pl];
+        auto diff_at = [&](uint32_t tr, int t) -> uint64_t {
+            const uint32_t p = tr + cbrv(t, G::LOGE) * G::T;
+            const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
+            if (canon) {
+                const uint64_t a = ac[j < (uint32_t)N ? j : j - N];
+                const uint64_t xr = j < (uint32_t)N || a == 0 ? a : q - a;
+                return subq(xr, ac[p], q);
+            }
+            const uint64_t xr = j < (uint32_t)N ? ac[j] : red_q(q - ac[j - N], q, mu);
+            return subq(red_q(xr, q, mu), red_q(ac[p], q, mu), q);
+        };
+        uint64_t cv[CV ? G::E : 1];
+        if constexpr (CV) {
+#pragma unroll
+            for (int t = 0; t < G::E; ++t) cv[t] = diff_at(tau, t);
+        }
         for (int g = 0; g < level; ++g) {
             // row (pl, g): digit g of X^rot acc_pl - acc_pl (MSB digit first)
             const int row = pl * level + g;
@@ -113,33 +154,53 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
             W v[G::E];
             Tw<W> t0[PassTw<K, 0>::COUNT];
             load_tw<K, 0>(tr, A.twf, t0);
-            const uint64_t *ac = accs[pl];
             load_coeffs<G::E>(v, (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
-                const uint32_t p = tr + cbrv(t, G::LOGE) * G::T;
-                const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
-                const uint64_t xr = j < (uint32_t)N ? ac[j] : red_q(q - ac[j - N], q, mu);
-                const uint64_t c = subq(red_q(xr, q, mu), red_q(ac[p], q, mu), q);
-                uint64_t d = (c >> shift) & mask;
-                if (d > half) d = red_q(q - (base - d), q, mu);
+                uint64_t d = ((CV ? cv[CV ? t : 0] : diff_at(tr, t)) >> shift) & mask;
+                if (d > half) d = small_base ? q - (base - d) : red_q(q - (base - d), q, mu);
                 return d;
             });
             fwd_pass<K, 0, false>(v, t0, A.ar);
             fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
+            // raw output (< 4q) times a canonical key: a valid Montgomery pair
+            if constexpr (XACC) {
+                // the other half's terms accumulate here and cross once per step
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) {
+                    const W own = A.ar.mont(v[e], (W)kv[0][e]), oth = A.ar.mont(v[e], (W)kv[1][e]);
+                    oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
+                    xacc[e] = g == 0 ? oth : A.ar.red2q(xacc[e] + oth);
+                }
+                if (g + 1 < level) __syncthreads();  // the exchange region is reused by the next level
+            } else {
+                // the other half may still read its exchange region (last pass)
+                if constexpr (ALIAS) __syncthreads();
+                W *const xo = xb(1 - pl);
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) {
+                    const uint32_t gi = gidx<K, G::NP - 1>(tr, e);
+                    const W own = A.ar.mont(v[e], (W)kv[0][e]);
+                    xo[gi] = A.ar.mont(v[e], (W)kv[1][e]);
+                    oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
+                }
+                __syncthreads();
+                const W *const xi = xb(pl);
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) oacc[e] = A.ar.red2q(oacc[e] + xi[gidx<K, G::NP - 1>(tr, e)]);
+                __syncthreads();  // the cross terms and the exchange regions are reused
+            }
+        }
+        if constexpr (XACC) {
+            uint32_t tx = tau;
+            asm volatile("" : "+v"(tx));
             // the other half may still read its exchange region (last pass)
             if constexpr (ALIAS) __syncthreads();
-            // raw output (< 4q) times a canonical key: a valid Montgomery pair
             W *const xo = xb(1 - pl);
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) {
-                const uint32_t gi = gidx<K, G::NP - 1>(tr, e);
-                const W own = A.ar.mont(v[e], (W)kv[0][e]);
-                xo[gi] = A.ar.mont(v[e], (W)kv[1][e]);
-                oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
-            }
+            for (int e = 0; e < G::E; ++e) xo[gidx<K, G::NP - 1>(tx, e)] = xacc[e];
             __syncthreads();
             const W *const xi = xb(pl);
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) oacc[e] = A.ar.red2q(oacc[e] + xi[gidx<K, G::NP - 1>(tr, e)]);
+            for (int e = 0; e < G::E; ++e) oacc[e] = A.ar.red2q(oacc[e] + xi[gidx<K, G::NP - 1>(tx, e)]);
             __syncthreads();  // the cross terms and the exchange regions are reused
         }
         // component pl: inverse, then acc_pl = mod_add(inv, red_q(acc_pl))
@@ -148,10 +209,12 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
         uint64_t *ap = accs[pl];
         inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
                                                       [&](uint32_t gi, uint64_t x) -> uint64_t {
-                                                          ap[gi] = addq(x, red_q(ap[gi], q, mu), q);
+                                                          const uint64_t a = ap[gi];
+                                                          ap[gi] = addq(x, canon ? a : red_q(a, q, mu), q);
                                                           return 0;
                                                       });
         __syncthreads();
+        canon = true;
     }
     for (uint32_t i = threadIdx.x; i < 2u * N; i += THREADS) gacc[i] = accs[i / N][i % N];
 }
