@@ -219,6 +219,175 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
     for (uint32_t i = threadIdx.x; i < 2u * N; i += THREADS) gacc[i] = accs[i / N][i % N];
 }
 
+// k = 1 on two CUs per ciphertext (small batches: the one-workgroup kernel
+// above leaves most CUs idle and is bound by its one CU's VALU).  Workgroup
+// (ct, h) owns accumulator component h: it transforms the L digit rows of
+// X^rot acc_h - acc_h, accumulates their MAC terms for its own output
+// component (oacc) and for the partner's (xacc), hands xacc to the partner
+// through global memory, adds the partner's terms into oacc, inverts, and
+// updates acc_h in LDS.  One hand-off per step per direction.
+// Hand-off (MI355X_MICROARCH.md "inter-workgroup visibility", the sc1 form):
+// payload stored write-through (sc1, 8 B per lane), every storing wave
+// drains (vmcnt(0)), a workgroup barrier, ONE lane stores the flag (sc1) =
+// executed step + 1; the consumer's wave 0 polls that word relaxed (bounded,
+// s_sleep), a barrier, then every payload load is an sc1 load.  Payload
+// double-buffered by step parity: a workgroup rewrites parity p only after
+// the partner has published the next step, i.e. finished reading p.
+// Placement: partners are blocks b and b + 8 (the same XCD when blocks are
+// dealt round-robin over the 8 XCDs: speed only, not correctness).  One
+// workgroup per CU (dynamic LDS pad), and the host launches this only when
+// the whole grid is co-resident (grid <= CUs); a partner that never arrives
+// (co-residency broken by other work) ends the spin after ~1 s and the
+// ciphertext's accumulators are poisoned with ~0 (never a canonical value).
+typedef __attribute__((address_space(1))) uint64_t g64;
+typedef __attribute__((address_space(1))) uint32_t g32;
+struct BrPairX {
+    uint32_t *flag;  // [batch][2] executed-step epochs (zeroed before each launch)
+    uint64_t *buf;   // [batch][2 halves][2 parities][N] partner MAC terms (W words)
+};
+#ifndef FHE_BR_PAIR_LOGE
+#define FHE_BR_PAIR_LOGE 3
+#endif
+#ifndef FHE_BR_PAIR_LOGE_SMALL
+#define FHE_BR_PAIR_LOGE_SMALL 3
+#endif
+template <int LOGN>
+constexpr int br_pair_key() { return gk(LOGN, LOGN >= 12 ? FHE_BR_PAIR_LOGE : FHE_BR_PAIR_LOGE_SMALL); }
+constexpr int kBrPairPadLds = 16 * 1024;  // dynamic LDS: keeps a second workgroup off the CU
+template <int LOGN, typename W>
+__global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs D, NttArgs<W> A, BrPairX X,
+                                                                        uint32_t batch) {
+    constexpr int K = br_pair_key<LOGN>();
+    using G = Geo<K>;
+    constexpr int N = G::N, T = G::T;
+    constexpr bool CV = G::E <= 8;
+    __shared__ uint64_t acc[N];  // raw accumulator component h
+    __shared__ W lds[G::LW];     // NTT exchange
+    __shared__ uint32_t fail;
+    const uint32_t b = blockIdx.x, ct = (b >> 4) * 8 + (b & 7), pl = (b >> 3) & 1;
+    if (ct >= batch) return;  // whole workgroup (and its partner: same ct)
+    const uint32_t tau = threadIdx.x;
+    const uint64_t q = A.q64, mu = A.mu64;
+    uint64_t *gacc = D.acc + ((size_t)ct * 2 + pl) * N;
+    {
+        const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
+        for (uint32_t i = tau; i < (uint32_t)N; i += T) acc[i] = rotated_at(gacc, i, r0, N, q, mu);
+    }
+    if (tau == 0) fail = 0;
+    __syncthreads();
+    const int level = D.level;
+    const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    const bool small_base = base <= q;
+    const size_t ggsw_words = (size_t)2 * level * 2 * N;
+    const uint64_t *lwe_a = D.lwe_a + (size_t)ct * D.lwe_dim;
+    g32 *const myflag = (g32 *)(X.flag + (size_t)ct * 2 + pl);
+    g32 *const peerflag = (g32 *)(X.flag + (size_t)ct * 2 + (1 - pl));
+    g64 *const mybuf = (g64 *)(X.buf + ((size_t)ct * 2 + pl) * 2 * N);
+    g64 *const peerbuf = (g64 *)(X.buf + ((size_t)ct * 2 + (1 - pl)) * 2 * N);
+    bool canon = false;
+    uint32_t epoch = 0;
+    for (uint32_t step = 0; step < D.lwe_dim; ++step) {
+        const int32_t r = rot_amount(lwe_a[step], N, D.lwe_q);  // uniform, and equal in both halves
+        if (r == 0) continue;
+        const uint32_t rot = rot_norm(r, N);
+        const uint64_t *key = D.bsk + ggsw_words * step;
+        W oacc[G::E], xacc[G::E];
+        auto diff_at = [&](uint32_t tr, int t) -> uint64_t {  // as in k_br_persist
+            const uint32_t p = tr + cbrv(t, G::LOGE) * T;
+            const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
+            if (canon) {
+                const uint64_t a = acc[j < (uint32_t)N ? j : j - N];
+                const uint64_t xr = j < (uint32_t)N || a == 0 ? a : q - a;
+                return subq(xr, acc[p], q);
+            }
+            const uint64_t xr = j < (uint32_t)N ? acc[j] : red_q(q - acc[j - N], q, mu);
+            return subq(red_q(xr, q, mu), red_q(acc[p], q, mu), q);
+        };
+        uint64_t cv[CV ? G::E : 1];
+        if constexpr (CV) {
+#pragma unroll
+            for (int t = 0; t < G::E; ++t) cv[t] = diff_at(tau, t);
+        }
+        for (int g = 0; g < level; ++g) {
+            const int row = pl * level + g;
+            const uint32_t shift = uint32_t(level - 1 - g) * uint32_t(D.base_log);
+            uint64_t kv[2][G::E];
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const uint32_t gi = gidx<K, G::NP - 1>(tau, e);
+                kv[0][e] = key[((size_t)row * 2 + pl) * N + gi];
+                kv[1][e] = key[((size_t)row * 2 + (1 - pl)) * N + gi];
+            }
+            uint32_t tr = tau;
+            asm volatile("" : "+v"(tr));
+            W v[G::E];
+            Tw<W> t0[PassTw<K, 0>::COUNT];
+            load_tw<K, 0>(tr, A.twf, t0);
+            load_coeffs<G::E>(v, (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
+                uint64_t d = ((CV ? cv[CV ? t : 0] : diff_at(tr, t)) >> shift) & mask;
+                if (d > half) d = small_base ? q - (base - d) : red_q(q - (base - d), q, mu);
+                return d;
+            });
+            fwd_pass<K, 0, false>(v, t0, A.ar);
+            fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const W own = A.ar.mont(v[e], (W)kv[0][e]), oth = A.ar.mont(v[e], (W)kv[1][e]);
+                oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
+                xacc[e] = g == 0 ? oth : A.ar.red2q(xacc[e] + oth);
+            }
+            if (g + 1 < level) __syncthreads();  // the exchange region is reused by the next level
+        }
+        // publish xacc (parity of this step), then take the partner's
+        ++epoch;
+        const uint32_t par = (epoch & 1) * N;
+        {
+            uint32_t tx = tau;
+            asm volatile("" : "+v"(tx));
+#pragma unroll
+            for (int e = 0; e < G::E; ++e)
+                __hip_atomic_store(mybuf + par + gidx<K, G::NP - 1>(tx, e), (uint64_t)xacc[e], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        if (tau == 0) __hip_atomic_store(myflag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tau < 64) {  // wave 0 polls the partner's flag
+            bool ok = false;
+            for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+                if (__hip_atomic_load(peerflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) {
+                    ok = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!ok && tau == 0) fail = 1;
+        }
+        __syncthreads();
+        if (fail) break;  // workgroup-uniform
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+        uint32_t ti = tau;
+        asm volatile("" : "+v"(ti));
+#pragma unroll
+        for (int e = 0; e < G::E; ++e) {
+            const W x = (W)__hip_atomic_load(peerbuf + par + gidx<K, G::NP - 1>(ti, e), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            oacc[e] = A.ar.red2q(oacc[e] + x);
+        }
+        // component h: inverse, then acc_h = mod_add(inv, red_q(acc_h))
+        inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
+                                                [&](uint32_t gi, uint64_t x) -> uint64_t {
+                                                    const uint64_t a = acc[gi];
+                                                    acc[gi] = addq(x, canon ? a : red_q(a, q, mu), q);
+                                                    return 0;
+                                                });
+        __syncthreads();
+        canon = true;
+    }
+    const bool bad = fail != 0;
+    for (uint32_t i = tau; i < (uint32_t)N; i += T) gacc[i] = bad ? ~0ull : acc[i];
+}
+
 // GLWE dimension k >= 2 (K1 = k + 1 >= 3 accumulators): the same one-launch
 // structure, generic in K1.  A step has K1 L digit rows; P thread groups
 // transform them P at a time (row r0 + group), and every row's product with
@@ -395,6 +564,45 @@ static hipError_t br_dispatch(const Plan &p, int k1, const BrArgs &D, size_t bat
     case 12: return br_one<12, W>(p, k1, D, batch, A);
     default: return hipErrorInvalidValue;
     }
+}
+
+// Two-CU blind rotation (k = 1, N = 1024..4096): grid of 16 ceil(batch / 8)
+// blocks, taken only when that grid fits one block per CU.
+bool br_pair_supported(const Plan &p, int k1, size_t batch) {
+    if (p.wide || k1 != 2 || p.logn < 10 || p.logn > 12 || batch == 0) return false;
+    return 16 * ((batch + 7) / 8) <= (size_t)p.cus;
+}
+size_t br_pair_scratch_bytes(const Plan &p, size_t batch) {
+    return ((batch * 2 * 4 + 15) / 16) * 16 + batch * 2 * 2 * ((size_t)1 << p.logn) * 8;
+}
+template <int LOGN, typename W>
+static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A) {
+    const unsigned grid = (unsigned)(16 * ((batch + 7) / 8));
+    hipLaunchKernelGGL((k_br_pair<LOGN, W>), dim3(grid), dim3(Geo<br_pair_key<LOGN>()>::T), kBrPairPadLds, p.stream, D,
+                       A, X, (uint32_t)batch);
+    return hipGetLastError();
+}
+template <typename W>
+static hipError_t br_pair_dispatch(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch,
+                                   const NttArgs<W> &A) {
+    switch (p.logn) {
+    case 10: return br_pair_one<10, W>(p, D, X, batch, A);
+    case 11: return br_pair_one<11, W>(p, D, X, batch, A);
+    case 12: return br_pair_one<12, W>(p, D, X, batch, A);
+    default: return hipErrorInvalidValue;
+    }
+}
+hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
+                          const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q, size_t batch,
+                          void *scratch) {
+    if (!br_pair_supported(p, 2, batch)) return hipErrorInvalidValue;
+    const size_t fbytes = ((batch * 2 * 4 + 15) / 16) * 16;
+    hipError_t e = hipMemsetAsync(scratch, 0, fbytes, p.stream);  // the flags, every launch
+    if (e != hipSuccess) return e;
+    BrArgs D{acc, bsk, lwe_a, lwe_b, lwe_q, lwe_dim, level, base_log};
+    BrPairX X{(uint32_t *)scratch, (uint64_t *)((char *)scratch + fbytes)};
+    return p.word == 32 ? br_pair_dispatch<uint32_t>(p, D, X, batch, p.a32)
+                        : br_pair_dispatch<uint64_t>(p, D, X, batch, p.a64);
 }
 
 hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uint64_t *acc, const uint64_t *bsk,

@@ -193,10 +193,11 @@ def test_blind_rotate_vs_oracle(fg, n, q, bl, lv, dim):
                                               (4096, 40961, 5, 2, "compat", 1), (4096, P27, 9, 3, "negacyclic", 1)])
 def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q, bl, lv, mode, k):
     """Small batches take the single-launch blind rotation (ntt_br.hip,
-    accumulators in LDS for the whole loop; k = 1 and, with K1 = 3
-    accumulators, k = 2); FHE_BR_PERSIST_MAX=0 forces the per-step launches
-    (k = 1) or the composed steps (k = 2).  Both bit-exact with each other,
-    and rows vs the oracle (compat mode)."""
+    accumulators in LDS for the whole loop; k = 1 on two CUs per ciphertext
+    (k_br_pair) or, with FHE_BR_PAIR=0, on one (k_br_persist); k = 2 with K1 = 3
+    accumulators); FHE_BR_PERSIST_MAX=0 forces the per-step launches (k = 1)
+    or the composed steps (k = 2).  All bit-exact with each other, and rows vs
+    the oracle (compat mode)."""
     b, dim = 5, 24
     r = fg.PolynomialRing(n, q, mode=mode)
     be = fg.BootstrapEngine(r, bl, lv, k)
@@ -209,12 +210,15 @@ def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q,
     acc0 = rnd(74, q, b, k + 1, n)  # both components non-zero
     acc0[2, 0, :3] = [2**64 - 1, q, q + 1]  # raw words
     got = {}
-    for pmax in ("4096", "0"):
+    for pmax, pair in (("4096", "1"), ("4096", "0"), ("0", "1")):
         monkeypatch.setenv("FHE_BR_PERSIST_MAX", pmax)
+        monkeypatch.setenv("FHE_BR_PAIR", pair)
         acc = acc0.copy()
         be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
-        got[pmax] = acc
-    assert (got["4096"] == got["0"]).all()
+        got[pmax + pair] = acc
+    assert (got["40961"] == got["01"]).all()
+    assert (got["40960"] == got["01"]).all()
+    got["4096"] = got["40961"]
     if mode == "compat":
         t = oracle.NTT(n, q)
         for i in (0, 1, 2):
