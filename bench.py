@@ -492,8 +492,8 @@ BR_PRESETS = [
 ]
 
 
-def br_presets(fhe_gpu, dist, g, batches=(1, 64, 1024)):
-    """Latency (batch 1 and 64) and throughput (batch 1024) of one blind
+def br_presets(fhe_gpu, dist, g, batches=(1, 64, 8192)):
+    """Latency (batch 1 and 64) and throughput (batch 8192) of one blind
     rotation per ciphertext at the reference presets; the reference's target
     is < 20 ms per bootstrap (.kiro/specs/fhe-accelerate/requirements.md:146)."""
     out = {}

@@ -245,11 +245,14 @@ struct BrPairX {
     uint32_t *flag;  // [batch][2] executed-step epochs (zeroed before each launch)
     uint64_t *buf;   // [batch][2 halves][2 parities][N] partner MAC terms (W words)
 };
+// 4 coefficients per thread (N / 4 threads per workgroup): 12.0 / 29.6 ms for
+// the two presets and 4.3 ms for 64 ciphertexts at N = 1024, vs 14.0 / 31.9 /
+// 6.1 ms at 8 per thread (round 4).
 #ifndef FHE_BR_PAIR_LOGE
-#define FHE_BR_PAIR_LOGE 3
+#define FHE_BR_PAIR_LOGE 2
 #endif
 #ifndef FHE_BR_PAIR_LOGE_SMALL
-#define FHE_BR_PAIR_LOGE_SMALL 3
+#define FHE_BR_PAIR_LOGE_SMALL 2
 #endif
 template <int LOGN>
 constexpr int br_pair_key() { return gk(LOGN, LOGN >= 12 ? FHE_BR_PAIR_LOGE : FHE_BR_PAIR_LOGE_SMALL); }

@@ -8,13 +8,13 @@
 #
 # usage: bash tools/gpu_evidence.sh <tag> [workload ...]
 #   workloads: fwd_mul polymul q62_fwd_mul q62_polymul nega_fwd_mul
-#              nega_polymul ct_mul relin c5   (default: all)
+#              nega_polymul ct_mul relin c5 br   (default: all)
 # output: gpurun_out/evidence_<tag>/<workload>/summary.json (copy to profiles/)
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=$1; shift
-WLS=${*:-"fwd_mul polymul q62_fwd_mul q62_polymul nega_fwd_mul nega_polymul ct_mul relin c5"}
+WLS=${*:-"fwd_mul polymul q62_fwd_mul q62_polymul nega_fwd_mul nega_polymul ct_mul relin c5 br"}
 P27=132120577; P62=4611686018326724609
 BID=$(python3 -c "import sys; sys.path.insert(0, 'node-fhe-accelerate_amd'); import fhe_gpu; print(fhe_gpu.build_id())") || exit 1
 OUT=gpurun_out/evidence_$TAG
@@ -33,6 +33,7 @@ spec() {
     nega_polymul) echo "--only polymul --no-check --no-q62 --mode negacyclic|k_polymul=polymul,16384,65536,$P27,negacyclic";;
     ct_mul)       echo "--only ct_mul|k_ct_mul=ct_mul,16384,8192,$P27";;
     relin)        echo "--only relin|k_dmac=relin,16384,8192,$P27";;
+    br)           echo "--only br_presets|k_br_pair=br_pair,4096,64,1152921504606584833";;
     c5)           echo "--only c5|k_extprod2=extprod_B23_L1,16384,4096,$P62 k_extprod_acc=extprod_B15_L2,16384,4096,$P62";;
     *) return 1;;
   esac
