@@ -231,9 +231,14 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  * fhe_blind_rotate_batch   blind_rotate (:547-577) of acc in place, for each
  *   ciphertext c with its own LWE (lwe_a[c], lwe_b[c]) modulo lwe_q; bsk_ntt
  *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).  k = 1 with
- *   n <= 16384 runs fused (one launch, or per-step CMux launches); k = 2..16
- *   and n = 32768 / 65536 run composed step by step (one digit buffer for
- *   the whole loop, stream-ordered, no host synchronisation).
+ *   n <= 16384 runs fused: one launch for the whole loop at n = 512..4096
+ *   (two CUs per ciphertext while 16 * ceil(batch / 8) <= CUs, else one;
+ *   FHE_BR_PAIR=0 forces one), per-step CMux launches above; k = 2..16 and
+ *   n = 32768 / 65536 run composed step by step (one digit buffer for the
+ *   whole loop, stream-ordered, no host synchronisation).  The two-CU launch
+ *   needs its workgroup pairs co-resident: if other work on the device keeps
+ *   a partner off the GPU for ~1 s, that ciphertext's acc is filled with ~0
+ *   (never a canonical residue) instead of hanging.
  *   fhe_bootstrap_batch takes the same shapes.
  * fhe_sample_extract_batch sample_extract (:594-624): lwe_a [batch][k*n].
  * fhe_key_switch_batch     key_switch (:626-674): ksk_a [in_dim*level][out_dim]

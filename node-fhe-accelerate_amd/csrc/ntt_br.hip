@@ -52,9 +52,13 @@ struct BrArgs {
 #ifndef FHE_BR_XACC
 #define FHE_BR_XACC 1
 #endif
+#ifndef FHE_BR_LOGE_SMALL
+#define FHE_BR_LOGE_SMALL FHE_BR_LOGE
+#endif
 template <int LOGN>
 constexpr int br_key() {
-    return LOGN >= 12 ? gk(LOGN, FHE_BR_LOGE) : gk(LOGN, LOGN - 7 < FHE_BR_LOGE ? LOGN - 7 : FHE_BR_LOGE);
+    return LOGN >= 12 ? gk(LOGN, FHE_BR_LOGE)
+                      : gk(LOGN, LOGN - 7 < FHE_BR_LOGE_SMALL ? LOGN - 7 : FHE_BR_LOGE_SMALL);
 }
 template <int LOGN>
 constexpr int br_threads() { return 2 * Geo<br_key<LOGN>()>::T; }
