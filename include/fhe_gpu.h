@@ -233,9 +233,11 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).  k = 1 with
  *   n <= 16384 runs fused: one launch for the whole loop at n = 512..4096
  *   (two CUs per ciphertext while 16 * ceil(batch / 8) <= CUs, else one;
- *   FHE_BR_PAIR=0 forces one), per-step CMux launches above; k = 2..16 and
- *   n = 32768 / 65536 run composed step by step (one digit buffer for the
- *   whole loop, stream-ordered, no host synchronisation).  The two-CU launch
+ *   FHE_BR_PAIR=0 forces one), per-step CMux launches above; k = 2..4 run
+ *   as one launch where the k + 1 accumulators fit in LDS (n = 512 / 1024
+ *   with 64-bit words; n = 2048 for k <= 3 with 32-bit words); other
+ *   k <= 16 and n = 32768 / 65536 run composed step by step (one digit
+ *   buffer for the whole loop, stream-ordered, no host synchronisation).  The two-CU launch
  *   needs its workgroup pairs co-resident: if other work on the device keeps
  *   a partner off the GPU for ~1 s, that ciphertext's acc is filled with ~0
  *   (never a canonical residue) instead of hanging.

@@ -536,31 +536,58 @@ __global__ void __launch_bounds__(256) k_br_persist_k(BrArgs D, NttArgs<W> A) {
     for (uint32_t i = threadIdx.x; i < (uint32_t)(K1 * N); i += G::THREADS) gacc[i] = accs[i / N][i % N];
 }
 
-// k1 == 2: N = 512..4096; k1 == 3 (GLWE dimension 2): N = 512 / 1024 (and
-// 2048 with 32-bit words), where the K1 accumulators and both halves'
-// partial sums fit in LDS.
+// k1 == 2: N = 512..4096; k1 = 3..5 (GLWE dimension 2..4): N = 512..2048
+// wherever the K1 accumulators, the exchange regions and both groups'
+// partial sums fit in LDS (u64: k = 2..4 at N <= 1024; u32: k = 2, 3 at
+// N = 2048 too).
+constexpr int kBrK1Max = 5;
+template <int LOGN, typename W, int K1>
+constexpr bool brk_fits() {
+    return LOGN >= 9 && LOGN <= 11 && br_k_lds_bytes<LOGN, W, K1, br_k_logp<LOGN, W, K1>()>() <= 160 * 1024;
+}
+template <int LOGN, typename W>
+static bool brk_fits_rt(int k1) {
+    switch (k1) {
+    case 3: return brk_fits<LOGN, W, 3>();
+    case 4: return brk_fits<LOGN, W, 4>();
+    case 5: return brk_fits<LOGN, W, 5>();
+    default: return false;
+    }
+}
 bool br_persist_supported(const Plan &p, int k1) {
     if (p.wide) return false;
     if (k1 == 2) return p.logn >= 9 && p.logn <= 12;
-    if (k1 == 3) return p.logn >= 9 && (p.logn <= 10 || (p.logn == 11 && p.word == 32));
-    return false;
+    if (k1 < 3 || k1 > kBrK1Max) return false;
+    switch (p.logn) {
+    case 9: return p.word == 32 ? brk_fits_rt<9, uint32_t>(k1) : brk_fits_rt<9, uint64_t>(k1);
+    case 10: return p.word == 32 ? brk_fits_rt<10, uint32_t>(k1) : brk_fits_rt<10, uint64_t>(k1);
+    case 11: return p.word == 32 ? brk_fits_rt<11, uint32_t>(k1) : brk_fits_rt<11, uint64_t>(k1);
+    default: return false;
+    }
 }
 
+template <int LOGN, typename W, int K1>
+static hipError_t brk_launch(const Plan &p, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
+    if constexpr (brk_fits<LOGN, W, K1>()) {
+        constexpr int LP = br_k_logp<LOGN, W, K1>();
+        hipLaunchKernelGGL((k_br_persist_k<LOGN, W, K1, LP>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
+        return hipGetLastError();
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
 template <int LOGN, typename W>
 static hipError_t br_one(const Plan &p, int k1, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
-    if (k1 == 2) {
+    switch (k1) {
+    case 2:
         hipLaunchKernelGGL((k_br_persist<LOGN, W>), dim3((unsigned)batch), dim3(br_threads<LOGN>()), 0, p.stream, D,
                            A);
-    } else if constexpr (LOGN > 11) {
-        return hipErrorInvalidValue;
-    } else {
-        constexpr int LP = br_k_logp<LOGN, W, 3>();
-        if constexpr (br_k_lds_bytes<LOGN, W, 3, LP>() <= 160 * 1024)
-            hipLaunchKernelGGL((k_br_persist_k<LOGN, W, 3, LP>), dim3((unsigned)batch), dim3(256), 0, p.stream, D, A);
-        else
-            return hipErrorInvalidValue;
+        return hipGetLastError();
+    case 3: return brk_launch<LOGN, W, 3>(p, D, batch, A);
+    case 4: return brk_launch<LOGN, W, 4>(p, D, batch, A);
+    case 5: return brk_launch<LOGN, W, 5>(p, D, batch, A);
+    default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 template <typename W>
 static hipError_t br_dispatch(const Plan &p, int k1, const BrArgs &D, size_t batch, const NttArgs<W> &A) {

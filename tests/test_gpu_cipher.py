@@ -192,7 +192,11 @@ def test_blind_rotate_vs_oracle(fg, n, q, bl, lv, dim):
                                               # tfhe-128-balanced (Q_50_1) and tfhe-256-secure (Q_60_1)
                                               (2048, 1125899906826241, 15, 2, "compat", 1),
                                               (4096, 1152921504606584833, 10, 3, "compat", 1),
-                                              (4096, 40961, 5, 2, "compat", 1), (4096, P27, 9, 3, "negacyclic", 1)])
+                                              (4096, 40961, 5, 2, "compat", 1), (4096, P27, 9, 3, "negacyclic", 1),
+                                              # GLWE dimension 3 / 4 (K1 = 4 / 5 accumulators in LDS)
+                                              (512, 12289, 4, 3, "compat", 3), (1024, P62, 15, 2, "compat", 3),
+                                              (2048, 40961, 5, 2, "compat", 3), (512, 12289, 4, 3, "compat", 4),
+                                              (1024, P62, 23, 1, "compat", 4)])
 def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q, bl, lv, mode, k):
     """Small batches take the single-launch blind rotation (ntt_br.hip,
     accumulators in LDS for the whole loop; k = 1 on two CUs per ciphertext
