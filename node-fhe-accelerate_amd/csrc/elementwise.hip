@@ -100,6 +100,24 @@ k_addsub(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) c[n - 1] = addsub1(a[n - 1], b[n - 1], sub, m);
 }
 
+// RNS ring elementwise ops in one launch: limb blockIdx.y of [limbs][per]
+// words with that limb's constants; op 0 = pointwise product, 1 = add, 2 = sub.
+__global__ void __launch_bounds__(kBlock)
+k_ew_limbs(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *__restrict__ c, size_t per,
+           int op, const ModConsts *__restrict__ tab) {
+    const ModConsts m = tab[blockIdx.y];
+    const size_t o = (size_t)blockIdx.y * per, n2 = per / 2;  // per = batch N, even
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a + o) + i);
+        const u64x2 y = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(b + o) + i);
+        u64x2 z;
+        z.x = op == 0 ? modmul1(x.x, y.x, m) : addsub1(x.x, y.x, op == 2, m);
+        z.y = op == 0 ? modmul1(x.y, y.y, m) : addsub1(x.y, y.y, op == 2, m);
+        __builtin_nontemporal_store(z, reinterpret_cast<u64x2 *>(c + o) + i);
+    }
+}
+
 __global__ void __launch_bounds__(kBlock)
 k_neg(const uint64_t *__restrict__ a, uint64_t *__restrict__ c, size_t n, uint64_t q) {
     const size_t n2 = n / 2;
@@ -346,6 +364,15 @@ hipError_t launch_addsub(const ModConsts &m, const uint64_t *a, const uint64_t *
                          hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_addsub, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, b, c, n, sub, m);
+    return hipGetLastError();
+}
+hipError_t launch_ew_limbs(const ModConsts *tab, int limbs, const uint64_t *a, const uint64_t *b, uint64_t *c,
+                           size_t per, int op, hipStream_t s) {
+    if (per == 0) return hipSuccess;
+    if ((per & 1) || limbs < 1 || limbs > 65535) return hipErrorInvalidValue;
+    const size_t g = grid_for(per / 2), gpl = (g + limbs - 1) / limbs;  // about the usual grid in total
+    hipLaunchKernelGGL(k_ew_limbs, dim3((unsigned)(gpl < 1 ? 1 : gpl), (unsigned)limbs), dim3(kBlock), 0, s, a, b, c,
+                       per, op, tab);
     return hipGetLastError();
 }
 hipError_t launch_neg(uint64_t q, const uint64_t *a, uint64_t *c, size_t n, hipStream_t s) {

@@ -60,6 +60,14 @@ hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t b
 hipError_t launch_fwd_mul(const Plan &p, const uint64_t *a, const uint64_t *w, uint64_t *out, size_t batch);
 // c = inv(fwd(a) (.) fwd(b))  (PolynomialRing::multiply)
 hipError_t launch_polymul(const Plan &p, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
+// RNS ring in one launch (grid.y = limb): `limbs` contiguous [batch][N]
+// blocks, limb l with the transform constants tab[l] (a device array of
+// NttArgs<uint32_t> or NttArgs<uint64_t> per p.word); every limb shares p's
+// degree, word and laziness.  inv_limbs: inverse (b == nullptr) or polymul.
+hipError_t launch_fwd_limbs(const Plan &p, const void *tab, int limbs, const uint64_t *in, uint64_t *out,
+                            size_t batch);
+hipError_t launch_inv_limbs(const Plan &p, const void *tab, int limbs, const uint64_t *a, const uint64_t *b,
+                            uint64_t *c, size_t batch);
 // q >= 2^62 (Plan::wide), any N: op as launch_big
 hipError_t launch_wide(const Plan &p, int op, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t batch);
 // N > 2^kMaxFusedLogN: op 0 fwd, 1 fwd*R, 2 fwd (.) b, 3 inv, 4 polymul
@@ -148,6 +156,10 @@ hipError_t launch_modmul(const ModConsts &m, const uint64_t *a, const uint64_t *
 hipError_t launch_addsub(const ModConsts &m, const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n, int sub,
                          hipStream_t s);
 hipError_t launch_neg(uint64_t q, const uint64_t *a, uint64_t *c, size_t n, hipStream_t s);
+// RNS ring: pointwise product (op 0), add (1), sub (2) over [limbs][per] with
+// per-limb constants tab[limb] (device array), one launch.
+hipError_t launch_ew_limbs(const ModConsts *tab, int limbs, const uint64_t *a, const uint64_t *b, uint64_t *c,
+                           size_t per, int op, hipStream_t s);
 hipError_t launch_mul_scalar(const ModConsts &m, const uint64_t *a, uint64_t sc, uint64_t sc_shoup, uint64_t *c,
                              size_t n, hipStream_t s);
 hipError_t launch_ml_montmul(const uint64_t consts[7], const uint64_t *a, const uint64_t *b, uint64_t *c, size_t n,

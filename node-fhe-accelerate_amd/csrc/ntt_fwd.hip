@@ -21,8 +21,8 @@
 namespace FHE_NS {
 
 template <int LOGN, typename W, bool LAZY, int EPI>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
-k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
+__device__ __forceinline__ void ntt_fwd_body(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch,
+                                             const NttArgs<W> &A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
@@ -47,6 +47,20 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
             __builtin_nontemporal_store((uint64_t)x, dst + gidx<LOGN, G::NP - 1>(tau, e));
         }
     }
+}
+template <int LOGN, typename W, bool LAZY, int EPI>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
+    ntt_fwd_body<LOGN, W, LAZY, EPI>(in, out, batch, A);
+}
+// RNS ring (polynomial_ring.cpp:224-237) in one launch: limb blockIdx.y of
+// [limbs][batch][N], with that limb's transform constants from a table.
+template <int LOGN, typename W, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_ntt_fwd_limbs(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch,
+                const NttArgs<W> *__restrict__ tab) {
+    const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
+    ntt_fwd_body<LOGN, W, LAZY, 0>(in + o, out + o, batch, tab[blockIdx.y]);
 }
 
 #ifndef FHE_FWDMUL_PREFETCH
@@ -219,6 +233,43 @@ static hipError_t fwd_any(const Plan &p, const uint64_t *in, uint64_t *out, size
     if (p.word == 32)
         return fwd_dispatch<uint32_t>(p, p.a32, in, out, batch, epi, wv);
     return fwd_dispatch<uint64_t>(p, p.a64, in, out, batch, epi, wv);
+}
+
+template <int LOGN0, typename W, bool LAZY>
+static hipError_t fwd_limbs_one(const Plan &p, const void *tab, int limbs, const uint64_t *in, uint64_t *out,
+                                size_t batch) {
+    constexpr int LOGN = fwd_key<LOGN0, W>();
+    using G = Geo<LOGN>;
+    const size_t blocks = (batch + G::P - 1) / G::P;
+    hipLaunchKernelGGL((k_ntt_fwd_limbs<LOGN, W, LAZY>), dim3(blocks, limbs), dim3(G::THREADS), 0, p.stream, in, out,
+                       batch, static_cast<const NttArgs<W> *>(tab));
+    return hipGetLastError();
+}
+template <int LOGN, typename W>
+static hipError_t fwd_limbs_lazy(const Plan &p, const void *tab, int limbs, const uint64_t *in, uint64_t *out,
+                                 size_t batch) {
+    if constexpr (sizeof(W) == 4)
+        if (p.lazy) return fwd_limbs_one<LOGN, W, true>(p, tab, limbs, in, out, batch);
+    return fwd_limbs_one<LOGN, W, false>(p, tab, limbs, in, out, batch);
+}
+template <typename W>
+static hipError_t fwd_limbs_dispatch(const Plan &p, const void *tab, int limbs, const uint64_t *in, uint64_t *out,
+                                     size_t batch) {
+    switch (p.logn) {
+#define FHE_CASE(L) \
+    case L: return fwd_limbs_lazy<L, W>(p, tab, limbs, in, out, batch);
+        FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
+        FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
+#undef FHE_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+hipError_t launch_fwd_limbs(const Plan &p, const void *tab, int limbs, const uint64_t *in, uint64_t *out,
+                            size_t batch) {
+    if (p.wide || p.logn > kMaxFusedLogN || limbs < 1 || limbs > 65535) return hipErrorInvalidValue;
+    if (batch == 0) return hipSuccess;
+    return p.word == 32 ? fwd_limbs_dispatch<uint32_t>(p, tab, limbs, in, out, batch)
+                        : fwd_limbs_dispatch<uint64_t>(p, tab, limbs, in, out, batch);
 }
 
 hipError_t launch_fwd(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch, int epi) {

@@ -12,8 +12,8 @@
 namespace FHE_NS {
 
 template <int LOGN, typename W>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
-k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
+__device__ __forceinline__ void ntt_inv_body(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch,
+                                             const NttArgs<W> &A) {
     using G = Geo<LOGN>;
     __shared__ W lds_all[G::P * lds_elems<LOGN, W>()];
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = wg_poly<G>();
@@ -36,6 +36,19 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
         }
     }
     inv_poly_from_regs<LOGN>(lds, v, tau, out + poly * G::N, valid, A, A.ninv);
+}
+template <int LOGN, typename W>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch, NttArgs<W> A) {
+    ntt_inv_body<LOGN, W>(in, out, batch, A);
+}
+// RNS ring in one launch (k_ntt_fwd_limbs): limb blockIdx.y
+template <int LOGN, typename W>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_ntt_inv_limbs(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch,
+                const NttArgs<W> *__restrict__ tab) {
+    const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
+    ntt_inv_body<LOGN, W>(in + o, out + o, batch, tab[blockIdx.y]);
 }
 
 // Where fwd(a) waits while fwd(b) runs: 0 = VGPRs (small N), 1 = a second
@@ -124,9 +137,8 @@ template <int LOGN, typename W>
 constexpr int polymul2_pf() { return sizeof(W) == 8 ? FHE_PF_DUAL64 : polymul_pf<LOGN>(); }
 
 template <int LOGN, typename W, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
-k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
-          NttArgs<W> A) {
+__device__ __forceinline__ void polymul_body(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c,
+                                             size_t batch, const NttArgs<W> &A) {
     using G = Geo<LOGN>;
     constexpr int STASH = polymul_stash<LOGN, W>();
     __shared__ W lds_all[G::P * lds_elems<LOGN, W>() + (STASH == 1 ? G::P * G::N : 0)];
@@ -184,6 +196,19 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     uint32_t ti = tau;
     if constexpr (sizeof(W) == 8 || STASH == 2) asm volatile("" : "+v"(ti));
     inv_poly_from_regs<LOGN, polymul_pf<LOGN>()>(lds, v, ti, crow, valid, A, A.ninv_r);
+}
+template <int LOGN, typename W, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
+k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
+          NttArgs<W> A) {
+    polymul_body<LOGN, W, LAZY>(a, b, c, batch, A);
+}
+template <int LOGN, typename W, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
+k_polymul_limbs(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
+                const NttArgs<W> *__restrict__ tab) {
+    const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
+    polymul_body<LOGN, W, LAZY>(a + o, b + o, c + o, batch, tab[blockIdx.y]);
 }
 
 // Polymul with 32 coefficients per thread: fwd(a) and fwd(b) run in
@@ -260,10 +285,30 @@ k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint6
 #endif
     polymul2_one<LOGN, W, LAZY>(lds, tau, a, b, c, poly, A);
 }
+template <int LOGN, typename W, bool LAZY>
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+k_polymul2_limbs(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
+                 const NttArgs<W> *__restrict__ tab) {
+    __shared__ W lds[lds_elems<LOGN, W>()];
+    const size_t poly = blockIdx.x;
+    if (poly >= batch) return;
+    const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
+    polymul2_one<LOGN, W, LAZY>(lds, threadIdx.x, a + o, b + o, c + o, poly, tab[blockIdx.y]);
+}
 
+// tab != nullptr: the RNS form, `limbs` limbs of [batch][N] each in one launch
+// (grid.y = limb), constants from tab[limb].
 template <int LOGN, typename W>
 static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, const uint64_t *a, const uint64_t *b,
-                          uint64_t *c, size_t batch) {
+                          uint64_t *c, size_t batch, const NttArgs<W> *tab = nullptr, int limbs = 1) {
+    // one launch of kernel K (or of its limb form KL when tab is given)
+    auto go = [&](auto K, auto KL, size_t blocks, int threads, auto... args) -> hipError_t {
+        if (tab)
+            hipLaunchKernelGGL(KL, dim3((unsigned)blocks, (unsigned)limbs), dim3(threads), 0, s, args..., tab);
+        else
+            hipLaunchKernelGGL(K, dim3((unsigned)blocks), dim3(threads), 0, s, args..., A);
+        return hipGetLastError();
+    };
     bool lazy = false;
     if constexpr (sizeof(W) == 4) lazy = p.lazy;
     constexpr int PK = polymul_key<LOGN, W>();
@@ -272,32 +317,25 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
     if constexpr (polymul_dual<PK, W>()) {
         if (b) {
             if constexpr (sizeof(W) == 4) {
-                if (lazy) {
-                    hipLaunchKernelGGL((k_polymul2<PK, W, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b,
-                                       c, batch, A);
-                    return hipGetLastError();
-                }
+                if (lazy)
+                    return go(k_polymul2<PK, W, true>, k_polymul2_limbs<PK, W, true>, pblocks, GP::THREADS, a, b, c,
+                              batch);
             }
-                hipLaunchKernelGGL((k_polymul2<PK, W, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
-            return hipGetLastError();
+            return go(k_polymul2<PK, W, false>, k_polymul2_limbs<PK, W, false>, pblocks, GP::THREADS, a, b, c, batch);
         }
     } else {
         if (b && lazy) {
             if constexpr (sizeof(W) == 4)
-                hipLaunchKernelGGL((k_polymul<PK, W, true>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
-            return hipGetLastError();
+                return go(k_polymul<PK, W, true>, k_polymul_limbs<PK, W, true>, pblocks, GP::THREADS, a, b, c, batch);
+            return hipErrorInvalidValue;
         } else if (b) {
-            hipLaunchKernelGGL((k_polymul<PK, W, false>), dim3(pblocks), dim3(GP::THREADS), 0, s, a, b, c, batch, A);
-            return hipGetLastError();
+            return go(k_polymul<PK, W, false>, k_polymul_limbs<PK, W, false>, pblocks, GP::THREADS, a, b, c, batch);
         }
     }
-    {
-        constexpr int IK = inv_key<LOGN, W>();
-        using GI = Geo<IK>;
-        const size_t iblocks = (batch + GI::P - 1) / GI::P;
-        hipLaunchKernelGGL((k_ntt_inv<IK, W>), dim3(iblocks), dim3(GI::THREADS), 0, s, a, c, batch, A);
-    }
-    return hipGetLastError();
+    constexpr int IK = inv_key<LOGN, W>();
+    using GI = Geo<IK>;
+    const size_t iblocks = (batch + GI::P - 1) / GI::P;
+    return go(k_ntt_inv<IK, W>, k_ntt_inv_limbs<IK, W>, iblocks, GI::THREADS, a, c, batch);
 }
 
 template <typename W>
@@ -318,6 +356,32 @@ static hipError_t inv_any(const Plan &p, const uint64_t *a, const uint64_t *b, u
     if (p.word == 32)
         return inv_dispatch<uint32_t>(p, p.a32, a, b, c, batch);
     return inv_dispatch<uint64_t>(p, p.a64, a, b, c, batch);
+}
+
+template <typename W>
+static hipError_t inv_limbs_dispatch(const Plan &p, const void *tab, int limbs, const uint64_t *a, const uint64_t *b,
+                                     uint64_t *c, size_t batch) {
+    const NttArgs<W> *t = static_cast<const NttArgs<W> *>(tab);
+    const NttArgs<W> *A0;  // unused by the limb kernels (their constants come from tab)
+    if constexpr (sizeof(W) == 4) A0 = &p.a32;
+    else A0 = &p.a64;
+    switch (p.logn) {
+#define FHE_CASE(L) \
+    case L: return inv_one<L, W>(p, *A0, p.stream, a, b, c, batch, t, limbs);
+        FHE_CASE(2) FHE_CASE(3) FHE_CASE(4) FHE_CASE(5) FHE_CASE(6) FHE_CASE(7) FHE_CASE(8)
+        FHE_CASE(9) FHE_CASE(10) FHE_CASE(11) FHE_CASE(12) FHE_CASE(13) FHE_CASE(14)
+#undef FHE_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+// RNS ring: inverse (b == nullptr) or polymul of `limbs` limbs in one launch
+hipError_t launch_inv_limbs(const Plan &p, const void *tab, int limbs, const uint64_t *a, const uint64_t *b,
+                            uint64_t *c, size_t batch) {
+    if (p.wide || p.logn > kMaxFusedLogN || limbs < 1 || limbs > 65535) return hipErrorInvalidValue;
+    if (batch == 0) return hipSuccess;
+    if (b && c == b) { const uint64_t *t = a; a = b; b = t; }
+    return p.word == 32 ? inv_limbs_dispatch<uint32_t>(p, tab, limbs, a, b, c, batch)
+                        : inv_limbs_dispatch<uint64_t>(p, tab, limbs, a, b, c, batch);
 }
 
 hipError_t launch_inv(const Plan &p, const uint64_t *in, uint64_t *out, size_t batch) {

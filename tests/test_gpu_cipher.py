@@ -430,6 +430,47 @@ def test_rns_ring_device_and_errors(fg):
         fg.RNSPolynomialRing(n, [P27, 97])
 
 
+@pytest.mark.parametrize("ring", ["u32", "bfv-128-simd", "u64"])
+def test_rns_ring_single_launch(fg, monkeypatch, ring):
+    """Device-resident calls on a ring whose limbs share one kernel shape run
+    every op as ONE launch (grid.y = limb, per-limb constants); bit-exact
+    with the per-limb launches (FHE_RNS_ONE_LAUNCH=0) and with the oracle."""
+    import torch
+    from fhe_gpu import params as P
+
+    if ring == "u32":
+        n, moduli = 4096, [P27, 40961, 114689]
+    elif ring == "u64":  # 16384: the paired u64 polymul and the 32-per-thread forward
+        n, moduli = 16384, [P62, 1152921504606584833]
+    else:
+        ps = P.create_parameter_set(ring)
+        n, moduli = ps.poly_degree, list(ps.moduli)
+    b = 2
+    r = fg.RNSPolynomialRing(n, moduli)
+    x = np.stack([rnd(700 + i, q, b, n) for i, q in enumerate(moduli)])
+    y = np.stack([rnd(800 + i, q, b, n) for i, q in enumerate(moduli)])
+    x[0, 0, :2] = [2**64 - 1, moduli[0]]  # raw words (x mod q)
+    dx = torch.from_numpy(x.view(np.int64)).cuda()
+    dy = torch.from_numpy(y.view(np.int64)).cuda()
+    ops = {"fwd": lambda: r.forward_ntt(dx), "inv": lambda: r.inverse_ntt(dx), "mul": lambda: r.multiply(dx, dy),
+           "pw": lambda: r.pointwise_multiply(dx, dy), "add": lambda: r.add(dx, dy), "sub": lambda: r.subtract(dx, dy)}
+    got = {}
+    for one in ("1", "0"):
+        monkeypatch.setenv("FHE_RNS_ONE_LAUNCH", one)
+        for k, f in ops.items():
+            out = f()
+            torch.cuda.synchronize()
+            got[k + one] = out.cpu().numpy().view(np.uint64)
+    for k in ops:
+        assert (got[k + "1"] == got[k + "0"]).all(), k
+    for i, q in enumerate(moduli[:2]):
+        t = oracle.NTT(n, q)
+        assert (got["fwd1"][i] == t.forward(x[i])).all(), q
+        assert (got["mul1"][i] == t.polymul(x[i], y[i])).all(), q
+        assert (got["pw1"][i] == oracle.pointwise(q, x[i].ravel(), y[i].ravel()).reshape(b, n)).all(), q
+        assert (got["sub1"][i] == oracle.poly_sub(q, x[i].ravel(), y[i].ravel()).reshape(b, n)).all(), q
+
+
 # ------------------------------------------------------------ reference parameter presets
 def test_presets_bfv_rns_and_tfhe_balanced(fg):
     """bfv-128-simd's modulus chain as an RNS ring, and tfhe-128-balanced's
