@@ -184,9 +184,14 @@ int fhe_decompose_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level, const u
 /* ---- RNS multi-modulus ring (PolynomialRing(degree, moduli),
  * polynomial_ring.cpp:224-237): one transform context per modulus, all on
  * one stream.  RNS polynomials are modulus-major: [count][batch][n] (limb i
- * of every polynomial contiguous), so each limb is one launch over a
- * contiguous batch.  The reference's ring operations use moduli_[0] only;
- * these apply the operation to every limb. */
+ * of every polynomial contiguous).  FHE_DEVICE calls run each operation as
+ * ONE launch over all limbs (grid.y = limb, per-limb constants from device
+ * tables built at creation) when every limb shares the kernel shape (n <=
+ * 16384, q < 2^62, all limbs in 32-bit or all in 64-bit lanes, same
+ * laziness); otherwise, and for FHE_HOST calls (staged limb by limb), one
+ * launch per limb.  FHE_RNS_ONE_LAUNCH=0 forces one launch per limb.  The
+ * reference's ring operations use moduli_[0] only; these apply the
+ * operation to every limb. */
 typedef struct fhe_rns_ctx fhe_rns_ctx;
 int fhe_rns_ctx_create(uint32_t n, const uint64_t *moduli, uint32_t count, int mode, int device, fhe_rns_ctx **out);
 void fhe_rns_ctx_destroy(fhe_rns_ctx *rns);

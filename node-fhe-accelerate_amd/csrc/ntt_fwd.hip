@@ -56,11 +56,12 @@ k_ntt_fwd(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 // RNS ring (polynomial_ring.cpp:224-237) in one launch: limb blockIdx.y of
 // [limbs][batch][N], with that limb's transform constants from a table.
 template <int LOGN, typename W, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)  // no occupancy floor: RNS calls are small
 k_ntt_fwd_limbs(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch,
                 const NttArgs<W> *__restrict__ tab) {
     const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
-    ntt_fwd_body<LOGN, W, LAZY, 0>(in + o, out + o, batch, tab[blockIdx.y]);
+    const NttArgs<W> A = tab[blockIdx.y];
+    ntt_fwd_body<LOGN, W, LAZY, 0>(in + o, out + o, batch, A);
 }
 
 #ifndef FHE_FWDMUL_PREFETCH

@@ -44,11 +44,12 @@ k_ntt_inv(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t ba
 }
 // RNS ring in one launch (k_ntt_fwd_limbs): limb blockIdx.y
 template <int LOGN, typename W>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)  // no occupancy floor: RNS calls are small
 k_ntt_inv_limbs(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t batch,
                 const NttArgs<W> *__restrict__ tab) {
     const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
-    ntt_inv_body<LOGN, W>(in + o, out + o, batch, tab[blockIdx.y]);
+    const NttArgs<W> A = tab[blockIdx.y];  // uniform: loaded into SGPRs like the kernel-argument form
+    ntt_inv_body<LOGN, W>(in + o, out + o, batch, A);
 }
 
 // Where fwd(a) waits while fwd(b) runs: 0 = VGPRs (small N), 1 = a second
@@ -204,11 +205,12 @@ k_polymul(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64
     polymul_body<LOGN, W, LAZY>(a, b, c, batch, A);
 }
 template <int LOGN, typename W, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul_occ<LOGN, W>()))
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)  // no occupancy floor: RNS calls are small
 k_polymul_limbs(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
                 const NttArgs<W> *__restrict__ tab) {
     const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
-    polymul_body<LOGN, W, LAZY>(a + o, b + o, c + o, batch, tab[blockIdx.y]);
+    const NttArgs<W> A = tab[blockIdx.y];
+    polymul_body<LOGN, W, LAZY>(a + o, b + o, c + o, batch, A);
 }
 
 // Polymul with 32 coefficients per thread: fwd(a) and fwd(b) run in
@@ -286,14 +288,15 @@ k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint6
     polymul2_one<LOGN, W, LAZY>(lds, tau, a, b, c, poly, A);
 }
 template <int LOGN, typename W, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS)  // no occupancy floor: RNS calls are small
 k_polymul2_limbs(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
                  const NttArgs<W> *__restrict__ tab) {
     __shared__ W lds[lds_elems<LOGN, W>()];
     const size_t poly = blockIdx.x;
     if (poly >= batch) return;
     const size_t o = (size_t)blockIdx.y * batch * Geo<LOGN>::N;
-    polymul2_one<LOGN, W, LAZY>(lds, threadIdx.x, a + o, b + o, c + o, poly, tab[blockIdx.y]);
+    const NttArgs<W> A = tab[blockIdx.y];
+    polymul2_one<LOGN, W, LAZY>(lds, threadIdx.x, a + o, b + o, c + o, poly, A);
 }
 
 // tab != nullptr: the RNS form, `limbs` limbs of [batch][N] each in one launch
