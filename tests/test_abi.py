@@ -170,6 +170,9 @@ SCRATCH_FREE = [
     "k_ntt_fwd<14, unsigned int, true, 0>", "k_ntt_fwd<1294, unsigned long, ",
     "k_ntt_inv<14, unsigned int>", "k_ntt_inv<14, unsigned long>",
     "k_extprod_acc<", "k_extprod2<14, unsigned long>", "k_br_persist<", "k_decrypt<",
+    # round 4: the two-CU blind rotation, k = 2..4 single launch, the RNS limb kernels
+    "k_br_pair<", "k_br_persist_k<", "k_ntt_fwd_limbs<", "k_ntt_inv_limbs<", "k_polymul_limbs<",
+    "k_polymul2_limbs<",
 ]
 # Ratchet: kernels that still use scratch anywhere (small-degree u64 digit
 # kernels, the ciphertext-multiply stash); the count may only go down (95 in
@@ -298,3 +301,37 @@ def test_typescript_declarations_match_exports():
     assert not missing, missing
     absent = sorted(m for m in methods if m not in out["methods"])
     assert not absent, absent
+
+
+def test_profile_traffic_requires_exact_kernel_and_build(tmp_path, monkeypatch):
+    """bench.py attaches a PMC traffic figure only from a summary of the exact
+    kernel it launches on the exact build loaded: a stale
+    build id, a different instantiation or another workload is ignored."""
+    import json
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    bid = fhe_gpu.build_id()
+    sym = bench.BENCH_KERNELS["polymul/q27"]
+    wl = {"kernel": "polymul", "n": 16384, "batch": 65536, "q": bench.P27}
+
+    def put(name, **kw):
+        d = tmp_path / "profiles" / name
+        d.mkdir(parents=True)
+        s = {"build_id": bid, "kernel_name": sym, "hbm_traffic_bytes_per_launch": 1.0, "workload": dict(wl),
+             "generated": "2026-01-01T00:00:00Z", "kernel_trace_full_batch": {"avg_ns": 5e6}}
+        s.update(kw)
+        (d / "summary.json").write_text(json.dumps(s))
+
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    put("stale", build_id="0" * 16, hbm_traffic_bytes_per_launch=2.0, generated="2026-02-01T00:00:00Z")
+    put("other_kernel", kernel_name=sym.replace("true", "false"), hbm_traffic_bytes_per_launch=3.0,
+        generated="2026-02-01T00:00:00Z")
+    put("other_workload", workload=dict(wl, batch=8192), hbm_traffic_bytes_per_launch=4.0,
+        generated="2026-02-01T00:00:00Z")
+    assert bench.pmc_traffic("polymul", 16384, 65536, bench.P27) is None
+    put("match")
+    tr = bench.pmc_traffic("polymul", 16384, 65536, bench.P27)
+    assert tr is not None and tr[0] == 1.0 and tr[1].endswith("match/summary.json") and tr[2] == 5.0
