@@ -243,9 +243,15 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  *   with 64-bit words; n = 2048 for k <= 3 with 32-bit words); other
  *   k <= 16 and n = 32768 / 65536 run composed step by step (one digit
  *   buffer for the whole loop, stream-ordered, no host synchronisation).  The two-CU launch
- *   needs its workgroup pairs co-resident: if other work on the device keeps
- *   a partner off the GPU for ~1 s, that ciphertext's acc is filled with ~0
- *   (never a canonical residue) instead of hanging.
+ *   needs its workgroup pairs co-resident.  It is a cooperative launch
+ *   (grid checked against the device's occupancy), pair launches of one
+ *   process are serialised per device, and a workgroup whose partner does
+ *   not answer within FHE_BR_PAIR_TIMEOUT_US (default 20000 us; 0 simulates
+ *   a partner that never answers, for tests) gives its
+ *   ciphertext up: a repair pass enqueued behind the launch recomputes every
+ *   given-up ciphertext on one CU from a saved copy of its input, so the
+ *   result is exact in every case (no host synchronisation either way).
+ *   fhe_br_repair_count reports how many ciphertexts took the repair pass.
  *   fhe_bootstrap_batch takes the same shapes.
  * fhe_sample_extract_batch sample_extract (:594-624): lwe_a [batch][k*n].
  * fhe_key_switch_batch     key_switch (:626-674): ksk_a [in_dim*level][out_dim]
@@ -260,6 +266,12 @@ int fhe_blind_rotate_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t
                            uint64_t *acc, size_t batch, int where);
 int fhe_sample_extract_batch(fhe_ctx *ctx, uint32_t k, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
                              size_t batch, int where);
+/* Ciphertexts of this context's two-CU blind rotations that were recomputed
+ * by the repair pass since the context was created (a partner workgroup that
+ * was not co-resident in time; see fhe_blind_rotate_batch).  Waits for the
+ * context's stream.  No reference counterpart: blind_rotate
+ * (bootstrap_engine.cpp:547-577) is a sequential CPU loop. */
+int fhe_br_repair_count(fhe_ctx *ctx, uint64_t *count);
 int fhe_key_switch_batch(uint64_t q, uint32_t base_log, uint32_t level, uint32_t in_dim, uint32_t out_dim,
                          const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a, const uint64_t *lwe_b,
                          uint64_t *out_a, uint64_t *out_b, size_t batch, int where, int device, void *hip_stream);

@@ -96,12 +96,20 @@ hipError_t launch_cmux_rotate(const Plan &p, int k1, int level, int base_log, co
 // 512 <= N <= 2048 only (br_persist_supported); acc is updated in place.
 bool br_persist_supported(const Plan &p, int k1);
 // k = 1 on two CUs per ciphertext (N = 1024..4096, grid 16 ceil(batch / 8)
-// <= CUs); scratch: br_pair_scratch_bytes (flags zeroed by the launch).
+// <= CUs); scratch: br_pair_scratch_bytes (flags zeroed by the launch).  A
+// workgroup whose partner does not answer within timeout_ticks (100 MHz)
+// gives up on its ciphertext; the launch is followed by a repair pass
+// (k_br_persist) over the given-up ciphertexts, each counted in *repairs.
+struct BrPairOpts {
+    uint64_t timeout_ticks;
+    bool coop;                     // hipLaunchCooperativeKernel (grid checked against occupancy)
+    unsigned long long *repairs;   // device counter
+};
 bool br_pair_supported(const Plan &p, int k1, size_t batch);
 size_t br_pair_scratch_bytes(const Plan &p, size_t batch);
 hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q, size_t batch,
-                          void *scratch);
+                          void *scratch, const BrPairOpts &o);
 hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
                              const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q,
                              size_t batch);

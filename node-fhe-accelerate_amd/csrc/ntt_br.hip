@@ -40,6 +40,13 @@ struct BrArgs {
     uint64_t lwe_q;
     uint32_t lwe_dim;
     int level, base_log;
+    // input accumulators when they are not read from acc (k_br_pair's saved
+    // copy, for its repair pass)
+    const uint64_t *acc_in = nullptr;
+    // repair pass of k_br_pair (k_br_persist only): ciphertexts with
+    // only[ct] == 0 are skipped; each one run adds 1 to *repairs
+    const uint32_t *only = nullptr;
+    unsigned long long *repairs = nullptr;
 };
 
 // 8 coefficients per thread (N / 8 threads per half) from N = 1024, fewer
@@ -92,15 +99,20 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
     auto xb = [&](uint32_t h) -> W * { return ALIAS ? xlds + h * G::LW : xsep + h * N; };
     const uint32_t tau = threadIdx.x & (G::T - 1), pl = threadIdx.x >> G::LOGT;
     const size_t ct = blockIdx.x;
+    if (D.only) {  // repair pass: only the ciphertexts k_br_pair gave up on
+        if (D.only[ct] == 0) return;  // workgroup-uniform, before any barrier
+        if (threadIdx.x == 0) atomicAdd(D.repairs, 1ull);
+    }
     const uint64_t q = A.q64, mu = A.mu64;
     W *lds = xlds + pl * G::LW;
     uint64_t *gacc = D.acc + ct * 2 * N;
     {
         // acc <- X^-round(b 2N/q) acc   (k_rotate's map)
+        const uint64_t *gin = (D.acc_in ? D.acc_in : D.acc) + ct * 2 * N;
         const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
         for (uint32_t i = threadIdx.x; i < 2u * N; i += THREADS) {
             const uint32_t j = i / N, p = i % N;
-            accs[j][p] = rotated_at(gacc + (size_t)j * N, p, r0, N, q, mu);
+            accs[j][p] = rotated_at(gin + (size_t)j * N, p, r0, N, q, mu);
         }
     }
     __syncthreads();
@@ -233,22 +245,39 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
 // Hand-off (MI355X_MICROARCH.md "inter-workgroup visibility", the sc1 form):
 // payload stored write-through (sc1, 8 B per lane), every storing wave
 // drains (vmcnt(0)), a workgroup barrier, ONE lane stores the flag (sc1) =
-// executed step + 1; the consumer's wave 0 polls that word relaxed (bounded,
+// executed step + 1; the consumer's wave 0 polls that word (bounded,
 // s_sleep), a barrier, then every payload load is an sc1 load.  Payload
 // double-buffered by step parity: a workgroup rewrites parity p only after
 // the partner has published the next step, i.e. finished reading p.
 // Placement: partners are blocks b and b + 8 (the same XCD when blocks are
-// dealt round-robin over the 8 XCDs: speed only, not correctness).  One
-// workgroup per CU (dynamic LDS pad), and the host launches this only when
-// the whole grid is co-resident (grid <= CUs); a partner that never arrives
-// (co-residency broken by other work) ends the spin after ~1 s and the
-// ciphertext's accumulators are poisoned with ~0 (never a canonical value).
+// dealt round-robin over the 8 XCDs: speed only, not correctness).
+//
+// Co-residency is what the hand-off needs, and nothing on the device can
+// promise it once other work shares the GPU (another context's stream, a
+// second process).  So a partner that does not answer within the timeout
+// (s_memrealtime, 100 MHz) is never waited for: the workgroup publishes an
+// ABORT flag (its partner, if it ever runs, stops at its next poll), marks the
+// ciphertext in fail[], and stores nothing.  The kernel reads its input from a
+// saved copy (acc_in) and the host enqueues a repair pass right behind it
+// (k_br_persist, one workgroup per ciphertext, `only` = fail[]) that recomputes
+// every marked ciphertext from that copy -- so the result is exact whatever
+// the residency, and the repairs are counted (fhe_br_repair_count).
 typedef __attribute__((address_space(1))) uint64_t g64;
 typedef __attribute__((address_space(1))) uint32_t g32;
 struct BrPairX {
-    uint32_t *flag;  // [batch][2] executed-step epochs (zeroed before each launch)
-    uint64_t *buf;   // [batch][2 halves][2 parities][N] partner MAC terms (W words)
+    uint32_t *flag;     // [batch][2] executed-step epochs (zeroed before each launch)
+    uint32_t *fail;     // [batch] set by a workgroup that gave up (zeroed before each launch)
+    uint64_t *buf;      // [batch][2 halves][2 parities][N] partner MAC terms (W words)
+    uint64_t timeout;   // poll budget per hand-off, s_memrealtime ticks (100 MHz)
 };
+constexpr uint32_t kBrAbort = 0x80000000u;
+// Flag store / poll memory order.  0: relaxed agent-scope atomics ordered by
+// the drained write-through payload (the MICROARCH "sc1" form); 1: the flag
+// stored with release and polled with acquire semantics (agent scope) -- the
+// formal HIP memory-model form, which adds an L2 write-back per step.
+#ifndef FHE_BR_PAIR_ACQREL
+#define FHE_BR_PAIR_ACQREL 0
+#endif
 // 4 coefficients per thread (N / 4 threads per workgroup): 12.0 / 29.6 ms for
 // the two presets and 4.3 ms for 64 ciphertexts at N = 1024, vs 14.0 / 31.9 /
 // 6.1 ms at 8 per thread (round 4).
@@ -277,8 +306,9 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
     const uint64_t q = A.q64, mu = A.mu64;
     uint64_t *gacc = D.acc + ((size_t)ct * 2 + pl) * N;
     {
+        const uint64_t *gin = D.acc_in + ((size_t)ct * 2 + pl) * N;
         const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
-        for (uint32_t i = tau; i < (uint32_t)N; i += T) acc[i] = rotated_at(gacc, i, r0, N, q, mu);
+        for (uint32_t i = tau; i < (uint32_t)N; i += T) acc[i] = rotated_at(gin, i, r0, N, q, mu);
     }
     if (tau == 0) fail = 0;
     __syncthreads();
@@ -358,20 +388,31 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
-        if (tau == 0) __hip_atomic_store(myflag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tau < 64) {  // wave 0 polls the partner's flag
+        if (tau == 0)
+            __hip_atomic_store(myflag, epoch, FHE_BR_PAIR_ACQREL ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tau < 64) {  // wave 0 polls the partner's flag, for at most X.timeout
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             bool ok = false;
-            for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
-                if (__hip_atomic_load(peerflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) {
+            for (;;) {
+                const uint32_t f = __hip_atomic_load(peerflag, FHE_BR_PAIR_ACQREL ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if (f & kBrAbort) break;  // the partner gave up
+                if (f >= epoch && X.timeout != 0) {  // zero budget: the test's never-answering partner
                     ok = true;
                     break;
                 }
+                if (__builtin_amdgcn_s_memrealtime() - t0 >= X.timeout) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            if (!ok && tau == 0) fail = 1;
+            if (!ok && tau == 0) {
+                fail = 1;
+                __hip_atomic_store(myflag, kBrAbort | epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((g32 *)(X.fail + ct), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();
-        if (fail) break;  // workgroup-uniform
+        if (fail) return;  // workgroup-uniform: nothing stored, the repair pass recomputes ct
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
         uint32_t ti = tau;
         asm volatile("" : "+v"(ti));
@@ -391,8 +432,7 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         __syncthreads();
         canon = true;
     }
-    const bool bad = fail != 0;
-    for (uint32_t i = tau; i < (uint32_t)N; i += T) gacc[i] = bad ? ~0ull : acc[i];
+    for (uint32_t i = tau; i < (uint32_t)N; i += T) gacc[i] = acc[i];
 }
 
 // GLWE dimension k >= 2 (K1 = k + 1 >= 3 accumulators): the same one-launch
@@ -606,37 +646,71 @@ bool br_pair_supported(const Plan &p, int k1, size_t batch) {
     if (p.wide || k1 != 2 || p.logn < 10 || p.logn > 12 || batch == 0) return false;
     return 16 * ((batch + 7) / 8) <= (size_t)p.cus;
 }
+// scratch: flags [batch][2] u32 + fail [batch] u32 (16-byte aligned), the
+// saved input accumulators [batch][2][N], the hand-off buffers [batch][2][2][N]
+static size_t br_pair_flag_bytes(size_t batch) { return ((batch * 3 * 4 + 15) / 16) * 16; }
 size_t br_pair_scratch_bytes(const Plan &p, size_t batch) {
-    return ((batch * 2 * 4 + 15) / 16) * 16 + batch * 2 * 2 * ((size_t)1 << p.logn) * 8;
+    const size_t n = (size_t)1 << p.logn;
+    return br_pair_flag_bytes(batch) + batch * 2 * n * 8 + batch * 2 * 2 * n * 8;
 }
 template <int LOGN, typename W>
-static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A) {
+static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
+                              bool coop) {
     const unsigned grid = (unsigned)(16 * ((batch + 7) / 8));
-    hipLaunchKernelGGL((k_br_pair<LOGN, W>), dim3(grid), dim3(Geo<br_pair_key<LOGN>()>::T), kBrPairPadLds, p.stream, D,
-                       A, X, (uint32_t)batch);
-    return hipGetLastError();
+    const dim3 block(Geo<br_pair_key<LOGN>()>::T);
+    if (!coop) {
+        hipLaunchKernelGGL((k_br_pair<LOGN, W>), dim3(grid), block, kBrPairPadLds, p.stream, D, A, X, (uint32_t)batch);
+        return hipGetLastError();
+    }
+    // cooperative launch: the runtime checks the whole grid against the
+    // device's occupancy before it starts (hipErrorCooperativeLaunchTooLarge
+    // instead of a grid that can never be co-resident)
+    BrArgs d = D;
+    NttArgs<W> a = A;
+    BrPairX x = X;
+    uint32_t nb = (uint32_t)batch;
+    void *args[] = {&d, &a, &x, &nb};
+    return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W>, dim3(grid), block, args, kBrPairPadLds,
+                                      p.stream);
 }
 template <typename W>
 static hipError_t br_pair_dispatch(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch,
-                                   const NttArgs<W> &A) {
+                                   const NttArgs<W> &A, bool coop) {
     switch (p.logn) {
-    case 10: return br_pair_one<10, W>(p, D, X, batch, A);
-    case 11: return br_pair_one<11, W>(p, D, X, batch, A);
-    case 12: return br_pair_one<12, W>(p, D, X, batch, A);
+    case 10: return br_pair_one<10, W>(p, D, X, batch, A, coop);
+    case 11: return br_pair_one<11, W>(p, D, X, batch, A, coop);
+    case 12: return br_pair_one<12, W>(p, D, X, batch, A, coop);
     default: return hipErrorInvalidValue;
     }
 }
 hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q, size_t batch,
-                          void *scratch) {
+                          void *scratch, const BrPairOpts &o) {
     if (!br_pair_supported(p, 2, batch)) return hipErrorInvalidValue;
-    const size_t fbytes = ((batch * 2 * 4 + 15) / 16) * 16;
-    hipError_t e = hipMemsetAsync(scratch, 0, fbytes, p.stream);  // the flags, every launch
+    const size_t n = (size_t)1 << p.logn, fbytes = br_pair_flag_bytes(batch), abytes = batch * 2 * n * 8;
+    uint32_t *flag = (uint32_t *)scratch, *failw = flag + batch * 2;
+    uint64_t *acc_in = (uint64_t *)((char *)scratch + fbytes);
+    uint64_t *buf = acc_in + batch * 2 * n;
+    hipError_t e = hipMemsetAsync(scratch, 0, fbytes, p.stream);  // flags and fail words, every launch
+    if (e == hipSuccess) e = hipMemcpyAsync(acc_in, acc, abytes, hipMemcpyDeviceToDevice, p.stream);
     if (e != hipSuccess) return e;
     BrArgs D{acc, bsk, lwe_a, lwe_b, lwe_q, lwe_dim, level, base_log};
-    BrPairX X{(uint32_t *)scratch, (uint64_t *)((char *)scratch + fbytes)};
-    return p.word == 32 ? br_pair_dispatch<uint32_t>(p, D, X, batch, p.a32)
-                        : br_pair_dispatch<uint64_t>(p, D, X, batch, p.a64);
+    D.acc_in = acc_in;
+    BrPairX X{flag, failw, buf, o.timeout_ticks};
+    e = p.word == 32 ? br_pair_dispatch<uint32_t>(p, D, X, batch, p.a32, o.coop)
+                     : br_pair_dispatch<uint64_t>(p, D, X, batch, p.a64, o.coop);
+    if (e == hipErrorCooperativeLaunchTooLarge) {
+        // the grid cannot be co-resident on this device: every ciphertext
+        // goes to the repair pass (the one-CU kernel)
+        (void)hipGetLastError();
+        e = hipMemsetAsync(failw, 0x01, batch * 4, p.stream);
+    }
+    if (e != hipSuccess) return e;
+    // repair pass: the ciphertexts marked in fail[], from the saved input
+    BrArgs R = D;
+    R.only = failw;
+    R.repairs = o.repairs;
+    return p.word == 32 ? br_dispatch<uint32_t>(p, 2, R, batch, p.a32) : br_dispatch<uint64_t>(p, 2, R, batch, p.a64);
 }
 
 hipError_t launch_br_persist(const Plan &p, int k1, int level, int base_log, uint64_t *acc, const uint64_t *bsk,

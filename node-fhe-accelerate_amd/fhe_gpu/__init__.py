@@ -136,6 +136,7 @@ SIGNATURES = [
     ("fhe_blind_rotate_batch", C.c_int,
      [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint64, vp, vp, C.c_size_t, C.c_int]),
     ("fhe_sample_extract_batch", C.c_int, [vp, C.c_uint32, vp, vp, vp, C.c_size_t, C.c_int]),
+    ("fhe_br_repair_count", C.c_int, [vp, C.POINTER(C.c_uint64)]),
     ("fhe_key_switch_batch", C.c_int,
      [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp, C.c_size_t, C.c_int,
       C.c_int, vp]),
@@ -1131,6 +1132,14 @@ class BootstrapEngine:
         _check(lib().fhe_blind_rotate_batch(r._h, self.k, self.base_log, self.level, dim, bla.ptr, blb.ptr,
                                             lwe_q if lwe_q is not None else r.modulus, bk.ptr, ba.ptr, nb, w))
         return acc
+
+    def repair_count(self) -> int:
+        """Ciphertexts of this ring's two-CU blind rotations recomputed on one
+        CU because a partner workgroup was not co-resident in time
+        (fhe_br_repair_count; waits for the ring's stream)."""
+        v = C.c_uint64(0)
+        _check(lib().fhe_br_repair_count(self.ring._h, C.byref(v)))
+        return int(v.value)
 
     def bootstrap(self, lwe_a, lwe_b, bsk_ntt, test_poly, ksk_a, ksk_b, ks_base_log: int, ks_level: int,
                   lwe_q: Optional[int] = None):

@@ -232,6 +232,93 @@ def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q,
             assert (got["4096"][i] == exp).all(), i
 
 
+Q50 = 1125899906826241      # Q_50_1 (parameter_set.cpp), tfhe-128-balanced
+Q60 = 1152921504606584833    # Q_60_1, tfhe-256-secure
+
+
+@pytest.mark.parametrize("coop", ["1", "0"])
+@pytest.mark.parametrize("n,q,bl,lv", [(1024, P62, 23, 1), (2048, Q50, 15, 2), (4096, Q60, 10, 3)])
+def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop):
+    """k_br_pair with a zero poll budget: every workgroup that reaches a
+    hand-off before its partner gives its ciphertext up (ABORT flag, fail
+    word, nothing stored), and the repair pass recomputes those from the
+    saved input -- the result still equals the one-CU kernel and the oracle,
+    and the repairs are counted."""
+    k, b, dim = 1, 6, 20
+    r = fg.PolynomialRing(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(171 + n, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a, lwe_b = rnd(172, q, b, dim), rnd(173, q, b)
+    lwe_a[1, :] = 0                 # every step skipped: no hand-off at all
+    acc0 = rnd(174, q, b, k + 1, n)
+    acc0[2, 0, :3] = [2**64 - 1, q, q + 1]  # raw words
+    monkeypatch.setenv("FHE_BR_PAIR", "0")
+    ref = acc0.copy()
+    be.blind_rotate(ref, lwe_a, lwe_b, bsk_ntt)
+    monkeypatch.setenv("FHE_BR_PAIR", "1")
+    monkeypatch.setenv("FHE_BR_PAIR_COOP", coop)
+    monkeypatch.setenv("FHE_BR_PAIR_TIMEOUT_US", "0")
+    before = be.repair_count()
+    acc = acc0.copy()
+    be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
+    assert (acc == ref).all()
+    assert be.repair_count() > before  # the timeout path ran
+    t = oracle.NTT(n, q)
+    for i in (0, 2):
+        assert (acc[i] == t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])).all(), i
+    # with the default budget the same call needs no repair
+    monkeypatch.delenv("FHE_BR_PAIR_TIMEOUT_US")
+    before = be.repair_count()
+    acc = acc0.copy()
+    be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
+    assert (acc == ref).all() and be.repair_count() == before
+
+
+@pytest.mark.parametrize("serial", ["1", "0"])
+def test_br_pair_concurrent_contexts(fg, monkeypatch, serial):
+    """Two contexts run two-CU blind rotations on two streams at once, with
+    grids that together need twice the CUs (2 x 256 workgroups at batch
+    128).  Serialised (the default) the launches queue behind each other;
+    with FHE_BR_PAIR_SERIAL=0 they may interleave, and a pair that is not
+    co-resident in time goes to the repair pass.  Either way both results
+    are exact (vs the one-CU kernel, and rows vs the oracle)."""
+    import torch
+
+    n, q, bl, lv, dim, k, b = 4096, Q60, 10, 3, 12, 1, 128
+    monkeypatch.setenv("FHE_BR_PAIR_SERIAL", serial)
+    monkeypatch.setenv("FHE_BR_PAIR_TIMEOUT_US", "3000")
+    rings = [fg.PolynomialRing(n, q) for _ in range(2)]
+    bes = [fg.BootstrapEngine(r, bl, lv, k) for r in rings]
+    bsk = rnd(181, q, dim, (k + 1) * lv, k + 1, n)
+
+    def T(x):
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
+
+    bsk_ntt = [T(be.prepare_ggsw(bsk)) for be in bes]
+    lwe_a = [rnd(182 + i, q, b, dim) for i in range(2)]
+    lwe_b = [rnd(184 + i, q, b) for i in range(2)]
+    acc0 = [rnd(186 + i, q, b, k + 1, n) for i in range(2)]
+    ins = [(T(lwe_a[i]), T(lwe_b[i])) for i in range(2)]
+    accs = [T(acc0[i]) for i in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    for i in range(2):
+        with torch.cuda.stream(streams[i]):
+            bes[i].blind_rotate(accs[i], ins[i][0], ins[i][1], bsk_ntt[i])
+    torch.cuda.synchronize()
+    monkeypatch.setenv("FHE_BR_PAIR", "0")
+    t = oracle.NTT(n, q)
+    for i in range(2):
+        ref = T(acc0[i])
+        bes[i].blind_rotate(ref, ins[i][0], ins[i][1], bsk_ntt[i])
+        torch.cuda.synchronize()
+        got = accs[i].cpu().numpy().view(np.uint64)
+        assert (got == ref.cpu().numpy().view(np.uint64)).all(), i
+        exp = t.blind_rotate(k, bl, lv, lwe_a[i][b - 1], int(lwe_b[i][b - 1]), q, bsk, acc0[i][b - 1])
+        assert (got[b - 1] == exp).all(), i
+
+
 @pytest.mark.parametrize("n,q,bl,lv,k", [(1024, P62, 15, 2, 2), (32768, P62, 23, 1, 1)])
 def test_cmux_composed_vs_oracle(fg, n, q, bl, lv, k):
     """CMux for k > 1 / N > 16384: ct0 + ExtProd(ct1 - ct0) composed."""
