@@ -189,10 +189,14 @@ hipError_t launch_br_add(const ModConsts &m, const uint64_t *cur, const uint64_t
 // sample_extract: glwe [batch][k+1][n] -> lwe_a [batch][k*n], lwe_b [batch]
 hipError_t launch_sample_extract(const ModConsts &m, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
                                  uint32_t n, uint32_t k, size_t batch, hipStream_t s);
-// LWE key switch (BootstrapEngine::key_switch)
+// LWE key switch (BootstrapEngine::key_switch); scratch of
+// key_switch_scratch_bytes (0: none needed) for the split partial sums.
+size_t key_switch_scratch_bytes(const ModConsts &m, uint32_t base_log, uint32_t level, uint32_t in_dim,
+                                uint32_t out_dim, size_t batch);
 hipError_t launch_key_switch(const ModConsts &m, uint32_t base_log, uint32_t level, uint32_t in_dim, uint32_t out_dim,
                              const uint64_t *ksk_a, const uint64_t *ksk_b, const uint64_t *lwe_a,
-                             const uint64_t *lwe_b, uint64_t *out_a, uint64_t *out_b, size_t batch, hipStream_t s);
+                             const uint64_t *lwe_b, uint64_t *out_a, uint64_t *out_b, size_t batch, void *scratch,
+                             hipStream_t s);
 hipError_t launch_decompose(const ModConsts &m, const uint64_t *poly, uint64_t *out, uint32_t n, size_t npoly,
                             uint32_t base_log, uint32_t level, hipStream_t s);
 

@@ -27,8 +27,16 @@
 #ifndef FHE_U64_NOVCC
 #define FHE_U64_NOVCC 1
 #endif
+#ifndef FHE_BR_STAMPS
+#define FHE_BR_STAMPS 0
+#endif
 #include "fhe_internal.hpp"
 #include "lwe_ops.hpp"
+#if FHE_BR_STAMPS
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#endif
 
 namespace FHE_NS {
 
@@ -235,6 +243,30 @@ __global__ void __launch_bounds__(br_threads<LOGN>()) k_br_persist(BrArgs D, Ntt
     for (uint32_t i = threadIdx.x; i < 2u * N; i += THREADS) gacc[i] = accs[i / N][i % N];
 }
 
+// LB forward transforms in lockstep (the digit rows of one decomposition
+// chunk): every twiddle is loaded once for all LB, the butterflies of the LB
+// transforms are independent (LB times the ILP), and one barrier per pass
+// exchange serves all of them (each has its own LDS region).  From pass PASS
+// on; the caller ran pass 0.
+template <int LOGN, int PASS, int LB, int PF, typename W>
+__device__ __forceinline__ void fwd_rest_lb(W *lds, W (&v)[LB][Geo<LOGN>::E], uint32_t tau,
+                                            const Tw<W> *__restrict__ tw, const Arith<W> &ar) {
+    using G = Geo<LOGN>;
+    if constexpr (PASS < G::NP) {
+        Tw<W> t[PassTw<LOGN, PASS>::COUNT];
+        load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);  // in flight across the exchange
+#pragma unroll
+        for (int l = 0; l < LB; ++l) lds_store<LOGN, PASS - 1>(lds + l * G::LW, v[l], tau);
+        __syncthreads();
+#pragma unroll
+        for (int l = 0; l < LB; ++l) lds_load<LOGN, PASS>(lds + l * G::LW, v[l], tau);
+        load_tw<LOGN, PASS, W, PF, 8>(tau, tw, t);
+#pragma unroll
+        for (int l = 0; l < LB; ++l) fwd_pass<LOGN, PASS, false>(v[l], t, ar);
+        fwd_rest_lb<LOGN, PASS + 1, LB, PF>(lds, v, tau, tw, ar);
+    }
+}
+
 // k = 1 on two CUs per ciphertext (small batches: the one-workgroup kernel
 // above leaves most CUs idle and is bound by its one CU's VALU).  Workgroup
 // (ct, h) owns accumulator component h: it transforms the L digit rows of
@@ -269,6 +301,7 @@ struct BrPairX {
     uint32_t *fail;     // [batch] set by a workgroup that gave up (zeroed before each launch)
     uint64_t *buf;      // [batch][2 halves][2 parities][N] partner MAC terms (W words)
     uint64_t timeout;   // poll budget per hand-off, s_memrealtime ticks (100 MHz)
+    uint64_t *stamps = nullptr;  // lab stamp build only: [grid][8] phase cycle sums
 };
 constexpr uint32_t kBrAbort = 0x80000000u;
 // Flag store / poll memory order.  0: relaxed agent-scope atomics ordered by
@@ -289,16 +322,63 @@ constexpr uint32_t kBrAbort = 0x80000000u;
 #endif
 template <int LOGN>
 constexpr int br_pair_key() { return gk(LOGN, LOGN >= 12 ? FHE_BR_PAIR_LOGE : FHE_BR_PAIR_LOGE_SMALL); }
-constexpr int kBrPairPadLds = 16 * 1024;  // dynamic LDS: keeps a second workgroup off the CU
+// Levels transformed in lockstep: up to 4, as many LDS exchange regions as
+// fit beside the accumulator (tfhe-256-secure, N = 4096 with 64-bit words:
+// 3 = its whole L).  Levels beyond LB run in further chunks of LB.
+#ifndef FHE_BR_PAIR_LB
+#define FHE_BR_PAIR_LB 4
+#endif
 template <int LOGN, typename W>
+constexpr int br_pair_lb() {
+    using G = Geo<br_pair_key<LOGN>()>;
+    int lb = G::T >= 1024 && FHE_BR_PAIR_LB > 3 ? 3 : FHE_BR_PAIR_LB;  // 128 VGPRs at 16 waves: spills at 4
+    while (lb > 1 && G::N * 8 + lb * G::LW * (int)sizeof(W) > 150 * 1024) --lb;
+    return lb;
+}
+// One workgroup per CU: the static LDS plus this dynamic pad exceeds half
+// the CU's 160 KiB.
+template <int LOGN, typename W, int LB>
+constexpr int br_pair_pad_lds() {
+    using G = Geo<br_pair_key<LOGN>()>;
+    const int st = G::N * 8 + LB * G::LW * (int)sizeof(W) + 16;
+    return st > 82 * 1024 ? 0 : 82 * 1024 - st;
+}
+// Lab diagnostic build (tools/lab/quick_variant2.sh ... -DFHE_BR_STAMPS=1):
+// wave 0 of every workgroup sums s_memtime differences per step phase and
+// the host prints the shares (FHE_BR_STAMPS=1 at run time).  Read shares,
+// never that build's run time.
+#ifndef FHE_BR_STAMPS
+#define FHE_BR_STAMPS 0
+#endif
+#if FHE_BR_STAMPS
+constexpr int kBrStampPhases = 8;
+__device__ __forceinline__ uint64_t br_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define BR_STAMP(ph)                                \
+    do {                                            \
+        const uint64_t t_ = br_stamp();             \
+        st_sum[ph] += t_ - st_last;                 \
+        st_last = t_;                               \
+    } while (0)
+#else
+#define BR_STAMP(ph) \
+    do {             \
+    } while (0)
+#endif
+template <int LOGN, typename W, int LB>
 __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs D, NttArgs<W> A, BrPairX X,
                                                                         uint32_t batch) {
     constexpr int K = br_pair_key<LOGN>();
     using G = Geo<K>;
     constexpr int N = G::N, T = G::T;
     constexpr bool CV = G::E <= 8;
-    __shared__ uint64_t acc[N];  // raw accumulator component h
-    __shared__ W lds[G::LW];     // NTT exchange
+    __shared__ uint64_t acc[N];      // raw accumulator component h
+    __shared__ W lds[LB * G::LW];    // NTT exchange, one region per lockstep level
     __shared__ uint32_t fail;
     const uint32_t b = blockIdx.x, ct = (b >> 4) * 8 + (b & 7), pl = (b >> 3) & 1;
     if (ct >= batch) return;  // whole workgroup (and its partner: same ct)
@@ -323,12 +403,16 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
     g64 *const peerbuf = (g64 *)(X.buf + ((size_t)ct * 2 + (1 - pl)) * 2 * N);
     bool canon = false;
     uint32_t epoch = 0;
+#if FHE_BR_STAMPS
+    uint64_t st_sum[kBrStampPhases] = {}, st_last = br_stamp();
+#endif
     for (uint32_t step = 0; step < D.lwe_dim; ++step) {
         const int32_t r = rot_amount(lwe_a[step], N, D.lwe_q);  // uniform, and equal in both halves
         if (r == 0) continue;
         const uint32_t rot = rot_norm(r, N);
         const uint64_t *key = D.bsk + ggsw_words * step;
         W oacc[G::E], xacc[G::E];
+        BR_STAMP(7);
         auto diff_at = [&](uint32_t tr, int t) -> uint64_t {  // as in k_br_persist
             const uint32_t p = tr + cbrv(t, G::LOGE) * T;
             const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
@@ -345,37 +429,56 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
 #pragma unroll
             for (int t = 0; t < G::E; ++t) cv[t] = diff_at(tau, t);
         }
-        for (int g = 0; g < level; ++g) {
-            const int row = pl * level + g;
-            const uint32_t shift = uint32_t(level - 1 - g) * uint32_t(D.base_log);
-            uint64_t kv[2][G::E];
+        BR_STAMP(0);
+        for (int g0 = 0; g0 < level; g0 += LB) {
+            // rows g0 .. g0 + LB - 1 of this half (digits MSB first); rows
+            // past `level` transform zeros and add nothing
+            uint64_t kv[LB][2][G::E];
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) {
-                const uint32_t gi = gidx<K, G::NP - 1>(tau, e);
-                kv[0][e] = key[((size_t)row * 2 + pl) * N + gi];
-                kv[1][e] = key[((size_t)row * 2 + (1 - pl)) * N + gi];
+            for (int l = 0; l < LB; ++l) {
+                const int row = pl * level + (g0 + l < level ? g0 + l : level - 1);
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) {
+                    const uint32_t gi = gidx<K, G::NP - 1>(tau, e);
+                    kv[l][0][e] = key[((size_t)row * 2 + pl) * N + gi];
+                    kv[l][1][e] = key[((size_t)row * 2 + (1 - pl)) * N + gi];
+                }
             }
             uint32_t tr = tau;
             asm volatile("" : "+v"(tr));
-            W v[G::E];
+            W v[LB][G::E];
             Tw<W> t0[PassTw<K, 0>::COUNT];
             load_tw<K, 0>(tr, A.twf, t0);
-            load_coeffs<G::E>(v, (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
-                uint64_t d = ((CV ? cv[CV ? t : 0] : diff_at(tr, t)) >> shift) & mask;
-                if (d > half) d = small_base ? q - (base - d) : red_q(q - (base - d), q, mu);
-                return d;
-            });
-            fwd_pass<K, 0, false>(v, t0, A.ar);
-            fwd_rest<K, 1, false, kPfSingle>(lds, v, tr, A.twf, A.ar);
 #pragma unroll
-            for (int e = 0; e < G::E; ++e) {
-                const W own = A.ar.mont(v[e], (W)kv[0][e]), oth = A.ar.mont(v[e], (W)kv[1][e]);
-                oacc[e] = g == 0 ? own : A.ar.red2q(oacc[e] + own);
-                xacc[e] = g == 0 ? oth : A.ar.red2q(xacc[e] + oth);
+            for (int l = 0; l < LB; ++l) {
+                const int g = g0 + l;
+                const uint32_t shift = g < level ? uint32_t(level - 1 - g) * uint32_t(D.base_log) : 0u;
+                load_coeffs<G::E>(v[l], (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
+                    if (g >= level) return 0;
+                    uint64_t d = ((CV ? cv[CV ? t : 0] : diff_at(tr, t)) >> shift) & mask;
+                    if (d > half) d = small_base ? q - (base - d) : red_q(q - (base - d), q, mu);
+                    return d;
+                });
+                fwd_pass<K, 0, false>(v[l], t0, A.ar);
             }
-            if (g + 1 < level) __syncthreads();  // the exchange region is reused by the next level
+            fwd_rest_lb<K, 1, LB, kPfSingle>(lds, v, tr, A.twf, A.ar);
+            BR_STAMP(1);
+#pragma unroll
+            for (int l = 0; l < LB; ++l) {
+                if (g0 + l >= level) break;  // uniform
+#pragma unroll
+                for (int e = 0; e < G::E; ++e) {
+                    const W own = A.ar.mont(v[l][e], (W)kv[l][0][e]), oth = A.ar.mont(v[l][e], (W)kv[l][1][e]);
+                    oacc[e] = g0 + l == 0 ? own : A.ar.red2q(oacc[e] + own);
+                    xacc[e] = g0 + l == 0 ? oth : A.ar.red2q(xacc[e] + oth);
+                }
+            }
+            if (g0 + LB < level) __syncthreads();  // the exchange regions are reused by the next chunk
+            BR_STAMP(2);
         }
-        // publish xacc (parity of this step), then take the partner's
+        // publish xacc (parity of this step), then take the partner's.
+        // (Publishing it before the own terms are accumulated measured 5 %
+        // slower at tfhe-256-secure, round 5.)
         ++epoch;
         const uint32_t par = (epoch & 1) * N;
         {
@@ -388,6 +491,7 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
+        BR_STAMP(3);
         if (tau == 0)
             __hip_atomic_store(myflag, epoch, FHE_BR_PAIR_ACQREL ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -413,6 +517,7 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         }
         __syncthreads();
         if (fail) return;  // workgroup-uniform: nothing stored, the repair pass recomputes ct
+        BR_STAMP(4);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
         uint32_t ti = tau;
         asm volatile("" : "+v"(ti));
@@ -422,6 +527,7 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
                                              __HIP_MEMORY_SCOPE_AGENT);
             oacc[e] = A.ar.red2q(oacc[e] + x);
         }
+        BR_STAMP(5);
         // component h: inverse, then acc_h = mod_add(inv, red_q(acc_h))
         inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
                                                 [&](uint32_t gi, uint64_t x) -> uint64_t {
@@ -431,7 +537,12 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
                                                 });
         __syncthreads();
         canon = true;
+        BR_STAMP(6);
     }
+#if FHE_BR_STAMPS
+    if (tau == 0 && X.stamps)
+        for (int ph = 0; ph < kBrStampPhases; ++ph) X.stamps[(size_t)b * kBrStampPhases + ph] = st_sum[ph];
+#endif
     for (uint32_t i = tau; i < (uint32_t)N; i += T) gacc[i] = acc[i];
 }
 
@@ -653,13 +764,14 @@ size_t br_pair_scratch_bytes(const Plan &p, size_t batch) {
     const size_t n = (size_t)1 << p.logn;
     return br_pair_flag_bytes(batch) + batch * 2 * n * 8 + batch * 2 * 2 * n * 8;
 }
-template <int LOGN, typename W>
-static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
-                              bool coop) {
+template <int LOGN, typename W, int LB>
+static hipError_t br_pair_lb_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
+                                 bool coop) {
+    constexpr int PAD = br_pair_pad_lds<LOGN, W, LB>();
     const unsigned grid = (unsigned)(16 * ((batch + 7) / 8));
     const dim3 block(Geo<br_pair_key<LOGN>()>::T);
     if (!coop) {
-        hipLaunchKernelGGL((k_br_pair<LOGN, W>), dim3(grid), block, kBrPairPadLds, p.stream, D, A, X, (uint32_t)batch);
+        hipLaunchKernelGGL((k_br_pair<LOGN, W, LB>), dim3(grid), block, PAD, p.stream, D, A, X, (uint32_t)batch);
         return hipGetLastError();
     }
     // cooperative launch: the runtime checks the whole grid against the
@@ -670,8 +782,26 @@ static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, 
     BrPairX x = X;
     uint32_t nb = (uint32_t)batch;
     void *args[] = {&d, &a, &x, &nb};
-    return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W>, dim3(grid), block, args, kBrPairPadLds,
-                                      p.stream);
+    return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W, LB>, dim3(grid), block, args, PAD, p.stream);
+}
+// Lockstep width for `level` levels: the LB <= br_pair_lb() with the fewest
+// idle (zero) transforms, the widest among equals.
+template <int LOGN, typename W>
+static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
+                              bool coop) {
+    constexpr int LM = br_pair_lb<LOGN, W>();
+    int lb = 1, best = 1 << 30;
+    for (int c = 1; c <= LM; ++c) {
+        const int work = (D.level + c - 1) / c * c;
+        if (work <= best) best = work, lb = c;
+    }
+    switch (lb) {
+    case 4: if constexpr (LM >= 4) return br_pair_lb_one<LOGN, W, 4>(p, D, X, batch, A, coop); else break;
+    case 3: if constexpr (LM >= 3) return br_pair_lb_one<LOGN, W, 3>(p, D, X, batch, A, coop); else break;
+    case 2: if constexpr (LM >= 2) return br_pair_lb_one<LOGN, W, 2>(p, D, X, batch, A, coop); else break;
+    default: break;
+    }
+    return br_pair_lb_one<LOGN, W, 1>(p, D, X, batch, A, coop);
 }
 template <typename W>
 static hipError_t br_pair_dispatch(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch,
@@ -697,8 +827,35 @@ hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc,
     BrArgs D{acc, bsk, lwe_a, lwe_b, lwe_q, lwe_dim, level, base_log};
     D.acc_in = acc_in;
     BrPairX X{flag, failw, buf, o.timeout_ticks};
+#if FHE_BR_STAMPS
+    const size_t grid = 16 * ((batch + 7) / 8);
+    const char *sv = std::getenv("FHE_BR_STAMPS");
+    if (sv && sv[0] == '1' && hipMalloc(&X.stamps, grid * kBrStampPhases * 8) == hipSuccess)
+        (void)hipMemsetAsync(X.stamps, 0, grid * kBrStampPhases * 8, p.stream);
+#endif
     e = p.word == 32 ? br_pair_dispatch<uint32_t>(p, D, X, batch, p.a32, o.coop)
                      : br_pair_dispatch<uint64_t>(p, D, X, batch, p.a64, o.coop);
+#if FHE_BR_STAMPS
+    if (X.stamps) {
+        std::vector<uint64_t> h(grid * kBrStampPhases);
+        (void)hipStreamSynchronize(p.stream);
+        (void)hipMemcpy(h.data(), X.stamps, h.size() * 8, hipMemcpyDeviceToHost);
+        double sum[kBrStampPhases] = {}, tot = 0;
+        size_t used = 0;
+        for (size_t w = 0; w < grid; ++w) {
+            if (h[w * kBrStampPhases + 6] == 0) continue;
+            ++used;
+            for (int ph = 0; ph < kBrStampPhases; ++ph) sum[ph] += (double)h[w * kBrStampPhases + ph];
+        }
+        for (int ph = 0; ph < kBrStampPhases; ++ph) tot += sum[ph];
+        static const char *nm[kBrStampPhases] = {"diff", "fwd", "mac", "publish", "poll", "payload", "inverse", "step"};
+        std::fprintf(stderr, "[br stamps] N=%u level=%d workgroups=%zu cycles/wg=%.0f:", 1u << p.logn, level, used,
+                     used ? tot / used : 0.0);
+        for (int ph = 0; ph < kBrStampPhases; ++ph) std::fprintf(stderr, " %s %.1f%%", nm[ph], tot ? 100 * sum[ph] / tot : 0.0);
+        std::fprintf(stderr, "\n");
+        (void)hipFree(X.stamps);
+    }
+#endif
     if (e == hipErrorCooperativeLaunchTooLarge) {
         // the grid cannot be co-resident on this device: every ciphertext
         // goes to the repair pass (the one-CU kernel)

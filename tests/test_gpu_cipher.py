@@ -429,6 +429,30 @@ def test_key_switch_vs_oracle(fg, q, bl, lv):
         assert int(ob[i]) == eb, i
 
 
+@pytest.mark.parametrize("b", [1, 3, 17])
+@pytest.mark.parametrize("q,bl,lv,in_dim,out_dim", [(Q60, 10, 3, 4096, 300), (Q50, 15, 2, 2048, 130),
+                                                    (P27, 4, 7, 1024, 257)])
+def test_key_switch_split_vs_oracle(fg, q, bl, lv, in_dim, out_dim, b):
+    """The deferred-reduction key switch at the TFHE presets' shapes (k N
+    input coefficients, (B, L) of the bootstrap key) for 1, 3 and 17
+    ciphertexts: one, four or sixteen ciphertexts per workgroup, the (i, l)
+    entries split over many workgroups with partial sums, the 96-bit
+    accumulator reduced once -- bit-exact vs the reference's per-term
+    remainder loop (oracle)."""
+    ksk_a = rnd(301 + bl, q, in_dim * lv, out_dim)
+    ksk_b = rnd(302 + bl, q, in_dim * lv)
+    lwe_a = rnd(303 + b, q, b, in_dim)
+    lwe_b = rnd(304 + b, q, b)
+    lwe_a[0, : in_dim // 2] = 0          # half the digits zero (the reference's skip)
+    if b > 1:
+        lwe_a[1, :] = q - 1              # every digit at its maximum
+    oa, ob = fg.BootstrapEngine.key_switch(q, bl, lv, ksk_a, ksk_b, lwe_a, lwe_b)
+    for i in range(b):
+        ea, eb = oracle.key_switch(q, bl, lv, ksk_a, ksk_b, lwe_a[i], int(lwe_b[i]))
+        assert (oa[i] == ea).all(), i
+        assert int(ob[i]) == eb, i
+
+
 def test_bootstrap_pipeline_device(fg):
     """blind_rotate -> sample_extract -> key_switch on device tensors equals
     the oracle's bootstrap_with_test_poly sequence (:676-708)."""
