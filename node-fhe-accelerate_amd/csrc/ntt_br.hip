@@ -481,6 +481,11 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         // slower at tfhe-256-secure, round 5.)
         ++epoch;
         const uint32_t par = (epoch & 1) * N;
+        // (Data-tagged granules -- each word canonical with epoch mod 4 in its
+        // top bits, polled by the lane that needs it, no drain or flag --
+        // measured 3-5 % slower on all three presets, round 5: the partner's
+        // stores take as long to become visible either way, and 16 waves
+        // polling four words per lane load the CU's memory queue.)
         {
             uint32_t tx = tau;
             asm volatile("" : "+v"(tx));
