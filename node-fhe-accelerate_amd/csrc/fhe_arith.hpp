@@ -142,6 +142,18 @@ __device__ __forceinline__ uint64_t sub_add64(uint64_t a, uint64_t b, uint64_t c
 #define FHE_RED64_BORROW 0
 #endif
 
+// The reference's 64-bit primes, all of the form q = 2^k - d with d < 2^32
+// (parameter_set.cpp:22-42, cpp/tests/test_harness.h:143-147).  A kernel
+// instantiated for one of them (key bits 12-13) computes the Shoup remainder's
+// h q mod 2^64 as (h << k) - h d: two 32-bit multiplies instead of three.
+struct SparsePrime { uint64_t q; uint32_t d, k; };
+constexpr SparsePrime kSparsePrimes[4] = {
+    {0, 0, 0},
+    {4611686018326724609ull, 3u * (1u << 25) - 1u, 62},  // 2^62 - (3 2^25 - 1)
+    {1152921504606584833ull, (1u << 18) - 1u, 60},       // Q_60_1 = 2^60 - 2^18 + 1
+    {1125899906826241ull, (1u << 14) - 1u, 50},          // Q_50_1 = 2^50 - 2^14 + 1
+};
+
 // Twiddle with its Shoup companion w' = floor(w * 2^W / q).
 template <typename W> struct Tw { W w, wp; };
 // Two Shoup multipliers of a stage-0 butterfly that folds a scaling into
@@ -160,9 +172,12 @@ struct Arith {
     W q, q2;      // q, 2q
     W qinv;       // -q^-1 mod 2^W (Montgomery)
     W r2;         // R^2 mod q, R = 2^W
+    // index into kSparsePrimes when q is one of them (0: none); read by the
+    // host's dispatch only (ntt_core.hpp gk_sparse)
+    uint32_t sp;
 
     // x in [0, 2^W): x*w mod q, lazy result in [0, 2q)   (Shoup)
-    template <bool CHAIN = true>
+    template <bool CHAIN = true, int SP = 0>
     __device__ __forceinline__ W shoup(W x, W w, W wp) const {
         W h = mulhi(x, wp);
 #ifndef FHE_SHOUP_MAD
@@ -196,6 +211,19 @@ struct Arith {
         } else if constexpr (sizeof(W) == 4 && FHE_SHOUP_MAD) {
             // x*w - h*q (mod 2^32) as one v_mad_u64_u32: h*(2^32 - q) + x*w
             return (W)((uint64_t)h * (uint32_t)(0u - q) + (uint32_t)(x * w));
+        } else if constexpr (sizeof(W) == 8 && SP != 0) {
+            // q = 2^k - d (kSparsePrimes[SP]): -(h q) = h d - (h << k) =
+            // h0 d + ((h1 d - (h0 << (k - 32))) << 32)  (mod 2^64)
+            constexpr uint32_t d = kSparsePrimes[SP].d, sk = kSparsePrimes[SP].k - 32;
+            const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32);
+            // h0 d as one v_mad_u64_u32 (d in an SGPR): the C form lets LLVM
+            // split it into a mul_lo / mul_hi pair (14194 vs 12999
+            // instructions in the q62 polymul)
+            uint64_t P, cy;
+            asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=&v"(P), "=&s"(cy) : "v"(h0), "s"(d));
+            (void)cy;
+            const uint32_t ph = (uint32_t)(P >> 32) + h1 * d - (h0 << sk);
+            return x * w + pair64((uint32_t)P, ph);
         } else if constexpr (sizeof(W) == 8 && FHE_SHOUP64_CHAIN && CHAIN) {
             return (W)lo_chain64(x, w, h);
         } else if constexpr (sizeof(W) == 8 && FHE_U64_NOVCC) {
@@ -242,11 +270,13 @@ struct Arith {
         (void)cy;
         return (uint32_t)r;
     }
-    __device__ __forceinline__ W shoup(W x, Tw<W> t) const { return shoup(x, t.w, t.wp); }
+    template <int SP = 0>
+    __device__ __forceinline__ W shoup(W x, Tw<W> t) const { return shoup<true, SP>(x, t.w, t.wp); }
     // Inverse butterflies keep the plain 64-bit form: with the mad chain the
     // compiler gives the non-negacyclic u64 inverse kernels a 256-byte stack
     // frame (k_ntt_inv / k_polymul <14, u64>).
-    __device__ __forceinline__ W shoup_inv(W x, Tw<W> t) const { return shoup<false>(x, t.w, t.wp); }
+    template <int SP = 0>
+    __device__ __forceinline__ W shoup_inv(W x, Tw<W> t) const { return shoup<false, SP>(x, t.w, t.wp); }
 
     // Montgomery: a*b*R^-1 mod q in [0, 2q); requires a*b < q*R.
     // 64-bit words (FHE_U64_NOVCC): the signed form (a*b - m*q) / R + q with
@@ -295,6 +325,7 @@ struct Arith {
         return (W)r;
     }
     // Harvey forward (Cooley-Tukey) butterfly, values in [0, 4q).
+    template <int SP = 0>
     __device__ __forceinline__ void ct(W &x, W &y, Tw<W> t) const {
         W a = red2q(x);
         if constexpr (sizeof(W) == 4 && FHE_NEG_FWD_TW) {
@@ -302,7 +333,7 @@ struct Arith {
             x = a - nb;
             y = a + nb + q2;
         } else {
-            W b = shoup(y, t);
+            W b = shoup<SP>(y, t);
             x = a + b;
             y = sub2q(a, b);
         }
@@ -313,6 +344,7 @@ struct Arith {
         else return a - b + q2;
     }
     // Forward butterfly without reducing x: outputs grow by 2q per stage.
+    template <int SP = 0>
     __device__ __forceinline__ void ct_lazy(W &x, W &y, Tw<W> t) const {
         W a = x;
         if constexpr (sizeof(W) == 4 && FHE_NEG_FWD_TW) {
@@ -320,7 +352,7 @@ struct Arith {
             x = a - nb;
             y = a + nb + q2;
         } else {
-            W b = shoup(y, t);
+            W b = shoup<SP>(y, t);
             x = a + b;
             y = a - b + q2;
         }
@@ -328,25 +360,28 @@ struct Arith {
     // Stage-0 butterfly that also multiplies by R = 2^W (twiddle 1 -> R):
     // puts the transform in Montgomery form for a following pointwise
     // Montgomery product.  Outputs in [0, 4q) for any inputs < 2^W.
+    template <int SP = 0>
     __device__ __forceinline__ void ct_rscale(W &x, W &y, Scale<W> r) const {
-        W a = shoup(x, r.a);
-        W b = shoup(y, r.b);
+        W a = shoup<SP>(x, r.a);
+        W b = shoup<SP>(y, r.b);
         x = a + b;
         y = sub2q(a, b);
     }
     // Gentleman-Sande butterfly, values in [0, 2q).
+    template <int SP = 0>
     __device__ __forceinline__ void gs(W &x, W &y, Tw<W> t) const {
         W s = x + y;
         W d = sub2q(x, y);
         x = red2q(s);
-        y = shoup_inv(d, t);
+        y = shoup_inv<SP>(d, t);
     }
     // Last GS stage with the N^-1 scaling folded in (w = 1 at stage 0).
+    template <int SP = 0>
     __device__ __forceinline__ void gs_scaled(W &x, W &y, Scale<W> ninv) const {
         W s = x + y;
         W d = sub2q(x, y);
-        x = shoup_inv(s, ninv.a);
-        y = shoup_inv(d, ninv.b);
+        x = shoup_inv<SP>(s, ninv.a);
+        y = shoup_inv<SP>(d, ninv.b);
     }
 };
 

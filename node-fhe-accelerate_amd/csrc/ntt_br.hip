@@ -331,7 +331,11 @@ constexpr int br_pair_key() { return gk(LOGN, LOGN >= 12 ? FHE_BR_PAIR_LOGE : FH
 template <int LOGN, typename W>
 constexpr int br_pair_lb() {
     using G = Geo<br_pair_key<LOGN>()>;
-    int lb = G::T >= 1024 && FHE_BR_PAIR_LB > 3 ? 3 : FHE_BR_PAIR_LB;  // 128 VGPRs at 16 waves: spills at 4
+    // 128 VGPRs at 16 waves: LB = 4 spills; LB = 3 with 64-bit words spills
+    // 4 VGPRs and still measured 29.6 vs 31.0 ms (LB = 1) at
+    // tfhe-256-secure (round 5)
+    const int cap = G::T >= 1024 ? 3 : 4;
+    int lb = FHE_BR_PAIR_LB < cap ? FHE_BR_PAIR_LB : cap;
     while (lb > 1 && G::N * 8 + lb * G::LW * (int)sizeof(W) > 150 * 1024) --lb;
     return lb;
 }
@@ -370,6 +374,8 @@ __device__ __forceinline__ uint64_t br_stamp() {
     do {             \
     } while (0)
 #endif
+// (Prime-specialised arithmetic, ntt_core.hpp gk_sparse, measured 0 to +2 %
+// on the three presets, round 5: not used here.)
 template <int LOGN, typename W, int LB>
 __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs D, NttArgs<W> A, BrPairX X,
                                                                         uint32_t batch) {
@@ -771,7 +777,7 @@ size_t br_pair_scratch_bytes(const Plan &p, size_t batch) {
 }
 template <int LOGN, typename W, int LB>
 static hipError_t br_pair_lb_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
-                                 bool coop) {
+                                bool coop) {
     constexpr int PAD = br_pair_pad_lds<LOGN, W, LB>();
     const unsigned grid = (unsigned)(16 * ((batch + 7) / 8));
     const dim3 block(Geo<br_pair_key<LOGN>()>::T);
@@ -787,7 +793,8 @@ static hipError_t br_pair_lb_one(const Plan &p, const BrArgs &D, const BrPairX &
     BrPairX x = X;
     uint32_t nb = (uint32_t)batch;
     void *args[] = {&d, &a, &x, &nb};
-    return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W, LB>, dim3(grid), block, args, PAD, p.stream);
+    return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W, LB>, dim3(grid), block, args, PAD,
+                                      p.stream);
 }
 // Lockstep width for `level` levels: the LB <= br_pair_lb() with the fewest
 // idle (zero) transforms, the widest among equals.

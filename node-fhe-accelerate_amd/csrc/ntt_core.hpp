@@ -43,7 +43,14 @@ constexpr int kPadB[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 10, 10, 0};
 // (radix-32 passes, N/32 threads) with gk(logn, 5).
 constexpr int gk(int logn, int loge) { return logn | (loge << 8); }
 constexpr int gk_logn(int k) { return k & 0xff; }
-constexpr int gk_loge(int k) { return (k >> 8) ? (k >> 8) : ((k & 0xff) < 4 ? (k & 0xff) : 4); }
+constexpr int gk_loge(int k) { return ((k >> 8) & 0xf) ? ((k >> 8) & 0xf) : ((k & 0xff) < 4 ? (k & 0xff) : 4); }
+// Bits 12-13: one of the reference's sparse 64-bit primes q = 2^k - d
+// (fhe_arith.hpp kSparsePrimes; Arith::sp at run time), compiled in as
+// constants: the Shoup remainder's h q takes two multiplies instead of
+// three.  Only the kernels that gain are instantiated with it; every other
+// key leaves the bits clear.
+constexpr int gk_sparse(int k, int sel) { return k | (sel << 12); }
+constexpr int gk_sp(int k) { return (k >> 12) & 3; }
 
 // Pads for 32 coefficients per thread (tools/lab/lds_pads.py): i + (i >> (L-5))
 // is conflict-free for every pass layout at L = 11..14.
@@ -332,58 +339,11 @@ __device__ __forceinline__ void load_tw(uint32_t tau, const Tw<W> *__restrict__ 
 }
 
 // ---------------------------------------------------------------- passes
-// Forward (CT) butterflies of pass PASS: stages S..S+R-1 ascending.  LAZY:
-// no intermediate reduction (values grow by 2q per stage; valid when
-// (4 + 2L) q <= 2^W).
-// RS (pass 0 only): global stage 0 multiplies by R (ct_rscale).
-template <int LOGN, int PASS, bool LAZY, typename W, bool RS = false>
-__device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                         const Arith<W> &ar, Scale<W> rmod = Scale<W>{}) {
-    using P = PassTw<LOGN, PASS>;
-    constexpr int R = P::R, NU = P::NU;
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-#pragma unroll
-        for (int u = 0; u < NU; ++u)
-#pragma unroll
-            for (int tt = 0; tt < (1 << R); ++tt) {
-                if (tt & (1 << k)) continue;
-                const int e = tt + (u << R), e2 = e + (1 << k);
-                const Tw<W> w = t[P::slot(k, u, tt & ((1 << k) - 1))];
-                if (RS && PASS == 0 && k == 0) ar.ct_rscale(v[e], v[e2], rmod);
-                else if constexpr (LAZY) ar.ct_lazy(v[e], v[e2], w);
-                else ar.ct(v[e], v[e2], w);
-            }
-}
-
-// Inverse (GS) butterflies of pass PASS: stages S+R-1..S descending.  When
-// FOLD, global stage 0 (w = 1) applies the N^-1 (or N^-1 * R) scaling.
-template <int LOGN, int PASS, bool FOLD, typename W>
-__device__ __forceinline__ void inv_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                         const Arith<W> &ar, Scale<W> scale) {
-    using P = PassTw<LOGN, PASS>;
-    constexpr int S = P::S, R = P::R, NU = P::NU;
-#pragma unroll
-    for (int k = R - 1; k >= 0; --k)
-#pragma unroll
-        for (int u = 0; u < NU; ++u)
-#pragma unroll
-            for (int tt = 0; tt < (1 << R); ++tt) {
-                if (tt & (1 << k)) continue;
-                const int e = tt + (u << R), e2 = e + (1 << k);
-                if (FOLD && S + k == 0) ar.gs_scaled(v[e], v[e2], scale);
-                else ar.gs(v[e], v[e2], t[P::slot(k, u, tt & ((1 << k) - 1))]);
-            }
-}
-
-struct NoHook {
-    __device__ void operator()() const {}
-};
-
-// One stage (K) of a pass, forward (CT) / inverse (GS).
-template <int LOGN, int PASS, int K, bool LAZY, typename W>
+// One stage (K) of a pass, forward (CT) / inverse (GS).  RS (pass 0, stage
+// 0 only): multiply by R (ct_rscale) instead of the twiddle.
+template <int LOGN, int PASS, int K, bool LAZY, typename W, bool RS = false>
 __device__ __forceinline__ void fwd_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
-                                          const Arith<W> &ar) {
+                                          const Arith<W> &ar, Scale<W> rmod = Scale<W>{}) {
     using P = PassTw<LOGN, PASS>;
     constexpr int R = P::R, NU = P::NU;
 #pragma unroll
@@ -392,9 +352,12 @@ __device__ __forceinline__ void fwd_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)
         for (int tt = 0; tt < (1 << R); ++tt) {
             if (tt & (1 << K)) continue;
             const int e = tt + (u << R), e2 = e + (1 << K);
-            const Tw<W> w = t[P::slot(K, u, tt & ((1 << K) - 1))];
-            if constexpr (LAZY) ar.ct_lazy(v[e], v[e2], w);
-            else ar.ct(v[e], v[e2], w);
+            if constexpr (RS && PASS == 0 && K == 0) ar.template ct_rscale<gk_sp(LOGN)>(v[e], v[e2], rmod);
+            else {
+                const Tw<W> w = t[P::slot(K, u, tt & ((1 << K) - 1))];
+                if constexpr (LAZY) ar.template ct_lazy<gk_sp(LOGN)>(v[e], v[e2], w);
+                else ar.template ct<gk_sp(LOGN)>(v[e], v[e2], w);
+            }
         }
 }
 template <int LOGN, int PASS, int K, bool FOLD, typename W>
@@ -408,10 +371,49 @@ __device__ __forceinline__ void inv_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)
         for (int tt = 0; tt < (1 << R); ++tt) {
             if (tt & (1 << K)) continue;
             const int e = tt + (u << R), e2 = e + (1 << K);
-            if (FOLD && S + K == 0) ar.gs_scaled(v[e], v[e2], scale);
-            else ar.gs(v[e], v[e2], t[P::slot(K, u, tt & ((1 << K) - 1))]);
+            if constexpr (FOLD && S + K == 0) ar.template gs_scaled<gk_sp(LOGN)>(v[e], v[e2], scale);
+            else ar.template gs<gk_sp(LOGN)>(v[e], v[e2], t[P::slot(K, u, tt & ((1 << K) - 1))]);
         }
 }
+// Whole passes as compile-time stage sequences (a runtime stage loop that
+// the unroller gives up on indexes the twiddle and coefficient arrays
+// dynamically: scratch and s_set_gpr_idx).
+template <int LOGN, int PASS, int K, bool LAZY, bool RS, typename W>
+__device__ __forceinline__ void fwd_stages_from(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                                const Arith<W> &ar, Scale<W> rmod) {
+    if constexpr (K < PassTw<LOGN, PASS>::R) {
+        fwd_stage<LOGN, PASS, K, LAZY, W, RS>(v, t, ar, rmod);
+        fwd_stages_from<LOGN, PASS, K + 1, LAZY, RS>(v, t, ar, rmod);
+    }
+}
+template <int LOGN, int PASS, int K, bool FOLD, typename W>
+__device__ __forceinline__ void inv_stages_from(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                                const Arith<W> &ar, Scale<W> scale) {
+    if constexpr (K >= 0) {
+        inv_stage<LOGN, PASS, K, FOLD>(v, t, ar, scale);
+        inv_stages_from<LOGN, PASS, K - 1, FOLD>(v, t, ar, scale);
+    }
+}
+// Forward (CT) butterflies of pass PASS: stages S..S+R-1 ascending.  LAZY:
+// no intermediate reduction (values grow by 2q per stage; valid when
+// (4 + 2L) q <= 2^W).
+// RS (pass 0 only): global stage 0 multiplies by R (ct_rscale).
+template <int LOGN, int PASS, bool LAZY, typename W, bool RS = false>
+__device__ __forceinline__ void fwd_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                         const Arith<W> &ar, Scale<W> rmod = Scale<W>{}) {
+    fwd_stages_from<LOGN, PASS, 0, LAZY, RS>(v, t, ar, rmod);
+}
+// Inverse (GS) butterflies of pass PASS: stages S+R-1..S descending.  When
+// FOLD, global stage 0 (w = 1) applies the N^-1 (or N^-1 * R) scaling.
+template <int LOGN, int PASS, bool FOLD, typename W>
+__device__ __forceinline__ void inv_pass(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)[PassTw<LOGN, PASS>::COUNT],
+                                         const Arith<W> &ar, Scale<W> scale) {
+    inv_stages_from<LOGN, PASS, PassTw<LOGN, PASS>::R - 1, FOLD>(v, t, ar, scale);
+}
+
+struct NoHook {
+    __device__ void operator()() const {}
+};
 
 // Staged twiddles (32 coefficients per thread, where a pass holds 31 twiddle
 // pairs per slot group): the twiddles of stage K+LA are issued while stage K
@@ -546,9 +548,9 @@ __device__ __forceinline__ void fwd_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::
             for (int tt = 0; tt < (1 << R); ++tt) {
                 if ((tt & (1 << k)) || (tt & ((1 << k) - 1)) != it.tl) continue;
                 const int e = tt + (it.u << R), e2 = e + (1 << k);
-                if constexpr (SK && k == 0) ar.ct_rscale(x[e], x[e2], rmod);
-                else if constexpr (LAZY) ar.ct_lazy(x[e], x[e2], b[I]);
-                else ar.ct(x[e], x[e2], b[I]);
+                if constexpr (SK && k == 0) ar.template ct_rscale<gk_sp(LOGN)>(x[e], x[e2], rmod);
+                else if constexpr (LAZY) ar.template ct_lazy<gk_sp(LOGN)>(x[e], x[e2], b[I]);
+                else ar.template ct<gk_sp(LOGN)>(x[e], x[e2], b[I]);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -574,8 +576,8 @@ __device__ __forceinline__ void inv_pass_stream(uint32_t tau, W (&v)[Geo<LOGN>::
             for (int tt = 0; tt < (1 << R); ++tt) {
                 if ((tt & (1 << k)) || (tt & ((1 << k) - 1)) != it.tl) continue;
                 const int e = tt + (it.u << R), e2 = e + (1 << k);
-                if constexpr (SK && k == 0) ar.gs_scaled(x[e], x[e2], scale);
-                else ar.gs(x[e], x[e2], b[I]);
+                if constexpr (SK && k == 0) ar.template gs_scaled<gk_sp(LOGN)>(x[e], x[e2], scale);
+                else ar.template gs<gk_sp(LOGN)>(x[e], x[e2], b[I]);
             }
         }
         __builtin_amdgcn_sched_barrier(0);

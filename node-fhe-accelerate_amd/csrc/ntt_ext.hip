@@ -294,12 +294,12 @@ k_extprod2(DmArgs D, NttArgs<W> A) {
     inv_poly2<LOGN, PF>(lds, v0, v1, ti, orow, orow + G::N, A, A.ninv);
 }
 
-// Relinearisation takes k_dmac MODE 1.  A 32-coefficient-per-thread kernel
-// (c2 low dwords and accumulator 1 in VGPRs, accumulator 0 in LDS, the next
-// level's keys in flight across each transform; 232 VGPRs, 8 waves per CU)
-// measured slower on MI355X: 9.03 vs 8.29 ms per 16,384 ciphertexts at
-// (L, B) = (7, 4) (round-4 A/B) -- the 16 waves of MODE 1 hide more of the
-// exchange barriers than the shorter transforms save.
+// Relinearisation takes k_dmac MODE 1.  Two 32-coefficient-per-thread
+// kernels (c2 low words and accumulator 1 in VGPRs, accumulator 0 in LDS; 8
+// waves per CU) measured slower on MI355X: single digit transforms 9.03 vs
+// 8.29 ms per 16,384 ciphertexts (round 4), digit levels in lockstep pairs
+// 4.67 vs 4.27 ms per 8,192 (round 5) -- the 16 waves of MODE 1 hide more of
+// the exchange barriers than the shorter transforms save.
 
 // FHE_EXT_ACC=0: multi-level external products at N = 16384 take k_dmac
 // (lab A/B against ntt_ext2.hip).
@@ -313,6 +313,19 @@ static hipError_t dmac_one(const NttArgs<W> &A, hipStream_t s, int k1, const DmA
     if (k1 != 2) return hipErrorInvalidValue;
     if constexpr (MODE == 0 && G::P == 1 && FHE_EXT2 && sizeof(W) == 8 && LOGN >= 12) {
         if (D.level == 1) {
+            if constexpr (LOGN == 14) {
+                // a sparse prime (ntt_core.hpp gk_sparse): C5 (23, 1) 8.1 -> 7.7 ms
+                // per 16,384 (round 5)
+                if (A.ar.sp == 1 || A.ar.sp == 2) {
+                    if (A.ar.sp == 1)
+                        hipLaunchKernelGGL((k_extprod2<gk_sparse(LOGN, 1), W>), dim3((unsigned)D.batch),
+                                           dim3(G::THREADS), 0, s, D, A);
+                    else
+                        hipLaunchKernelGGL((k_extprod2<gk_sparse(LOGN, 2), W>), dim3((unsigned)D.batch),
+                                           dim3(G::THREADS), 0, s, D, A);
+                    return hipGetLastError();
+                }
+            }
             hipLaunchKernelGGL((k_extprod2<LOGN, W>), dim3((unsigned)D.batch), dim3(G::THREADS), 0, s, D, A);
             return hipGetLastError();
         }

@@ -460,3 +460,52 @@ def test_negacyclic_mode_is_ring_product(fg, golden_dir):
         expect[0, 0] = (q - int(x[0, -1])) % q
         assert (r.multiply(x, X) == expect).all()
         assert (r.inverse_ntt(r.forward_ntt(x)) == x).all()
+
+
+# ------------------------------------------------------------ sparse primes
+def rnd(seed, q, *shape):
+    return oracle.splitmix_fill(seed, q, int(np.prod(shape))).reshape(shape)
+
+
+Q60 = 1152921504606584833        # Q_60_1 = 2^60 - 2^18 + 1
+Q_DENSE62 = 3458764513825652737  # 3 2^60 + 0x4e0001: 62 bits, not 2^k - d with d < 2^32
+
+
+@pytest.mark.parametrize("q", [P62, Q60])
+def test_sparse_prime_kernels_match_generic(fg, monkeypatch, q):
+    """The reference's 64-bit primes take prime-specialised kernels at
+    N = 16384 (fhe_arith.hpp kSparsePrimes: h q mod 2^64 as (h << k) - h d);
+    FHE_SPARSE=0 at context creation keeps the generic ones.  Both must agree
+    word for word on fwd, fwd*w, inverse, polymul and the external product
+    (levels 1 and 2), and rows match the oracle."""
+    n, b = 16384, 6
+    x, y = rnd(501, q, b, n), rnd(502, q, b, n)
+    x[0, :3] = [2**64 - 1, q, q + 1]  # raw words
+    glwe = rnd(503, q, b, 2, n)
+    out = {}
+    for sp in ("0", "1"):
+        monkeypatch.setenv("FHE_SPARSE", sp)
+        r = fg.PolynomialRing(n, q)
+        res = [r.forward_ntt(x), r.forward_ntt_mul(x, y), r.inverse_ntt(x), r.multiply(x, y)]
+        for bl, lv in ((23, 1), (15, 2)):
+            ggsw = rnd(504 + lv, q, 2 * lv, 2, n)
+            res.append(fg.ExternalProduct(r, ggsw, bl, lv)(glwe))
+        out[sp] = res
+    for a, c in zip(out["0"], out["1"]):
+        assert (a == c).all()
+    t = oracle.NTT(n, q)
+    assert (out["1"][3][[0, b - 1]] == t.polymul(x[[0, b - 1]], y[[0, b - 1]])).all()
+    assert (out["1"][1][[0, b - 1]] == t.fwd_mul(x[[0, b - 1]], y[[0, b - 1]])).all()
+
+
+def test_dense_62bit_prime_vs_oracle(fg):
+    """A 62-bit NTT prime far from any power of two: the generic 64-bit
+    kernels at N = 16384 (never the sparse ones) vs the oracle."""
+    n, q, b = 16384, Q_DENSE62, 3
+    r = fg.PolynomialRing(n, q)
+    t = oracle.NTT(n, q)
+    x, y = rnd(511, q, b, n), rnd(512, q, b, n)
+    assert (r.forward_ntt(x) == t.forward(x)).all()
+    assert (r.forward_ntt_mul(x, y) == t.fwd_mul(x, y)).all()
+    assert (r.multiply(x, y) == t.polymul(x, y)).all()
+    assert (r.inverse_ntt(x) == t.inverse(x)).all()
