@@ -453,6 +453,31 @@ def test_key_switch_split_vs_oracle(fg, q, bl, lv, in_dim, out_dim, b):
         assert int(ob[i]) == eb, i
 
 
+@pytest.mark.parametrize("name,n,q,bl,lv", [("tfhe-128-balanced", 2048, Q50, 15, 2),
+                                             ("tfhe-256-secure", 4096, Q60, 10, 3)])
+@pytest.mark.parametrize("b", [1, 5])
+def test_bootstrap_presets_vs_oracle(fg, name, n, q, bl, lv, b):
+    """fhe_bootstrap_batch (bootstrap_with_test_poly, bootstrap_engine.cpp:
+    684-711: blind rotation on two CUs per ciphertext, sample extract, key
+    switch back to the LWE dimension with the bootstrap's (B, L) as
+    generate_key_switch_key builds it, :367-420) at the reference presets'
+    (N, q, B, L), LWE dimension reduced to 12, vs the oracle."""
+    k, dim = 1, 12
+    r = fg.PolynomialRing(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    o = oracle.NTT(n, q)
+    bsk = rnd(601 + n, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a, lwe_b = rnd(602, q, b, dim), rnd(603, q, b)
+    lwe_a[0, 0] = 0  # a skipped step
+    tp = be.create_lookup_table(lambda x: (5 * x + 3) % 16, 16, 16)
+    ksk_a, ksk_b = rnd(604, q, k * n * lv, dim), rnd(605, q, k * n * lv)
+    oa, ob = be.bootstrap(lwe_a, lwe_b, bsk_ntt, tp, ksk_a, ksk_b, bl, lv)
+    for i in range(b):
+        ea, eb = o.bootstrap(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, tp, bl, lv, ksk_a, ksk_b)
+        assert (oa[i] == ea).all() and int(ob[i]) == eb, (name, i)
+
+
 def test_bootstrap_pipeline_device(fg):
     """blind_rotate -> sample_extract -> key_switch on device tensors equals
     the oracle's bootstrap_with_test_poly sequence (:676-708)."""
