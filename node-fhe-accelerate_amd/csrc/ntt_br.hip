@@ -296,6 +296,18 @@ __device__ __forceinline__ void fwd_rest_lb(W *lds, W (&v)[LB][Geo<LOGN>::E], ui
 // the residency, and the repairs are counted (fhe_br_repair_count).
 typedef __attribute__((address_space(1))) uint64_t g64;
 typedef __attribute__((address_space(1))) uint32_t g32;
+typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64x2v pair128(uint64_t a, uint64_t b) {
+    u64x2v v;
+    v.x = a;
+    v.y = b;
+    return v;
+}
+// 1: the hand-off payload as 16-byte sc1 stores / loads (lane-contiguous
+// word pairs); 0: 8-byte agent-scope atomics at the words' own positions
+#ifndef FHE_BR_PAIR_X16
+#define FHE_BR_PAIR_X16 1
+#endif
 struct BrPairX {
     uint32_t *flag;     // [batch][2] executed-step epochs (zeroed before each launch)
     uint32_t *fail;     // [batch] set by a workgroup that gave up (zeroed before each launch)
@@ -495,10 +507,21 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         {
             uint32_t tx = tau;
             asm volatile("" : "+v"(tx));
+            if constexpr (FHE_BR_PAIR_X16 && G::E >= 2 && G::E <= 8) {
+                // 16-byte sc1 stores, lane-contiguous pairs (the partner's lane
+                // tau reads exactly these words)
 #pragma unroll
-            for (int e = 0; e < G::E; ++e)
-                __hip_atomic_store(mybuf + par + gidx<K, G::NP - 1>(tx, e), (uint64_t)xacc[e], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                for (int e = 0; e < G::E; e += 2) {
+                    g64 *p = mybuf + par + 2 * ((e / 2) * T + tx);
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(pair128((uint64_t)xacc[e], (uint64_t)xacc[e + 1]))
+                                 : "memory");
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < G::E; ++e)
+                    __hip_atomic_store(mybuf + par + gidx<K, G::NP - 1>(tx, e), (uint64_t)xacc[e], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
@@ -532,11 +555,39 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
         uint32_t ti = tau;
         asm volatile("" : "+v"(ti));
+        if constexpr (FHE_BR_PAIR_X16 && G::E >= 2 && G::E <= 8) {
+            // the loads and their wait in ONE asm statement: the outputs exist
+            // for the compiler only once they have landed (an output the
+            // compiler spills between a load and a separate wait would be
+            // stored before it arrives)
+            u64x2v x[G::E / 2];
+            const g64 *p0 = peerbuf + par + 2 * ti;
+            if constexpr (G::E == 2) {
+                asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(x[0]) : "v"(p0) : "memory");
+            } else if constexpr (G::E == 4) {
+                asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %3, off sc1\n\t"
+                             "s_waitcnt vmcnt(0)"
+                             : "=&v"(x[0]), "=&v"(x[1]) : "v"(p0), "v"(p0 + 2 * T) : "memory");
+            } else {
+                static_assert(G::E == 8, "2, 4 or 8 words per lane");
+                asm volatile("global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %5, off sc1\n\t"
+                             "global_load_dwordx4 %2, %6, off sc1\n\tglobal_load_dwordx4 %3, %7, off sc1\n\t"
+                             "s_waitcnt vmcnt(0)"
+                             : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+                             : "v"(p0), "v"(p0 + 2 * T), "v"(p0 + 4 * T), "v"(p0 + 6 * T) : "memory");
+            }
 #pragma unroll
-        for (int e = 0; e < G::E; ++e) {
-            const W x = (W)__hip_atomic_load(peerbuf + par + gidx<K, G::NP - 1>(ti, e), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-            oacc[e] = A.ar.red2q(oacc[e] + x);
+            for (int e = 0; e < G::E; e += 2) {
+                oacc[e] = A.ar.red2q(oacc[e] + (W)x[e / 2].x);
+                oacc[e + 1] = A.ar.red2q(oacc[e + 1] + (W)x[e / 2].y);
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const W x = (W)__hip_atomic_load(peerbuf + par + gidx<K, G::NP - 1>(ti, e), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                oacc[e] = A.ar.red2q(oacc[e] + x);
+            }
         }
         BR_STAMP(5);
         // component h: inverse, then acc_h = mod_add(inv, red_q(acc_h))
