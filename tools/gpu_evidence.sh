@@ -48,7 +48,10 @@ for wl in $WLS; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d/trace -o run --output-format csv -- python3 $B \
     > $d/trace.log 2>&1 || { echo "$wl trace failed rc=$?"; tail -5 $d/trace.log; exit 1; }
   i=0
-  for ctr in FETCH_SIZE WRITE_SIZE "$SQ"; do
+  # relinearisation: L2 -> CU read requests and L2 hit/miss (the prepared
+  # key is re-read from L2 by every workgroup)
+  EXTRA=""; [ $wl = relin ] && EXTRA="TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum"
+  for ctr in FETCH_SIZE WRITE_SIZE "$SQ" ${EXTRA:+"$EXTRA"}; do
     i=$((i + 1))
     echo "$wl: pmc$i $(date +%T)" >> $OUT/progress.log
     timeout -s KILL 240 rocprofv3 --pmc $ctr -d $d/pmc_$i -o run --output-format csv -- python3 $B \

@@ -28,7 +28,7 @@ for q in [int(x) for x in args.qs.split(",")]:
     g = torch.Generator(device="cuda").manual_seed(7)
     a = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
     b = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
-    out = torch.empty_like(a)
+    out = torch.randint(0, q, (B, n), device="cuda", dtype=torch.int64, generator=g)
     ring = fhe_gpu.PolynomialRing(n, q, mode=args.mode)
     eps = {}
     for bl, lv in ((23, 1), (15, 2)):
@@ -53,7 +53,8 @@ for q in [int(x) for x in args.qs.split(",")]:
               "relin": lambda: eng.relinearize(c3, ek, out=c2)}[op]
         fn()
         torch.cuda.synchronize()
-        chk = int(out[:8].sum().item()) ^ int(out[-8:].sum().item())
+        res = {"ext1": gout, "ext2": gout, "relin": c2, "ct_mul": c3}.get(op, out)
+        chk = int(res.sum().item()) ^ int(res[-1].sum().item())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.steps):
