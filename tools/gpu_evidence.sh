@@ -33,6 +33,8 @@ spec() {
     nega_polymul) echo "--only polymul --no-check --no-q62 --mode negacyclic|k_polymul=polymul,16384,65536,$P27,negacyclic";;
     ct_mul)       echo "--only ct_mul|k_ct_mul=ct_mul,16384,8192,$P27";;
     relin)        echo "--only relin|k_dmac=relin,16384,8192,$P27";;
+    # (cooperative launch off under the profiler: rocprofv3 7.2 segfaults in
+    # its exit handlers after any hipLaunchCooperativeKernel; same kernel)
     br)           echo "--only br_presets|k_br_pair=br_pair,4096,64,1152921504606584833";;
     c5)           echo "--only c5|k_extprod2=extprod_B23_L1,16384,4096,$P62 k_extprod_acc=extprod_B15_L2,16384,4096,$P62";;
     *) return 1;;
@@ -44,6 +46,7 @@ for wl in $WLS; do
   args=${sp%%|*}; sums=${sp#*|}
   d=$OUT/$wl; mkdir -p $d
   B="bench.py --steps 10 --warmup 3 $args"
+  if [ $wl = br ]; then export FHE_BR_PAIR_COOP=0; else unset FHE_BR_PAIR_COOP; fi
   echo "$wl: trace $(date +%T)" | tee -a $OUT/progress.log
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d/trace -o run --output-format csv -- python3 $B \
     > $d/trace.log 2>&1 || { echo "$wl trace failed rc=$?"; tail -5 $d/trace.log; exit 1; }
