@@ -324,6 +324,9 @@ export declare class NttContext {
   constructor(degree: number, modulus: bigint | number, mode?: number, device?: number | number[]);
   info(): NttContextInfo;
   synchronize(): void;
+  /** Ciphertexts of two-CU blind rotations recomputed by the one-CU repair pass
+   * (a partner workgroup was not co-resident; results are exact either way). */
+  brRepairCount(): number;
   forward(a: Words, out?: Words): Words;
   inverse(a: Words, out?: Words): Words;
   polymul(a: Words, b: Words, out: Words): Words;
@@ -382,6 +385,7 @@ export declare class PolynomialEngine {
   relinearize(ct3: Words, rlk: Words, baseLog?: number, out?: Words): Words;
   multiplyRelin(ct1: Words, ct2: Words, rlk: Words, baseLog?: number): Words;
   blindRotate(acc: Words, lweA: Words, lweB: Words, bsk: Words, baseLog: number, level: number): Words;
+  brRepairCount(): number;
   info(): NttContextInfo;
 }
 

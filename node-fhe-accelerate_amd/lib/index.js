@@ -55,6 +55,8 @@ class PolynomialEngine {
   blindRotate(acc, lweA, lweB, bsk, baseLog, level) {
     return this.ctx.blindRotate(acc, lweA, lweB, bsk, baseLog, level);
   }
+  /** ciphertexts of two-CU blind rotations recomputed by the one-CU repair pass */
+  brRepairCount() { return this.ctx.brRepairCount(); }
   info() { return this.ctx.info(); }
 }
 

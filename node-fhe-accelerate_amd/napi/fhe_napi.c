@@ -1397,6 +1397,19 @@ static napi_value ctx_synchronize(napi_env env, napi_callback_info info) {
     return u;
 }
 
+/* ciphertexts of two-CU blind rotations recomputed by the repair pass (a
+   partner workgroup was not co-resident); synchronises the context */
+static napi_value ctx_br_repairs(napi_env env, napi_callback_info info) {
+    call k;
+    if (call_begin(env, info, 0, &k)) return NULL;
+    uint64_t n = 0;
+    pthread_mutex_lock(&k.k->mu);
+    int rc = fhe_br_repair_count(k.c, &n);
+    pthread_mutex_unlock(&k.k->mu);
+    if (rc) return throw_fhe(env, rc);
+    return make_i64(env, (int64_t)n);
+}
+
 static napi_value ctx_info(napi_env env, napi_callback_info info) {
     call k;
     if (call_begin(env, info, 0, &k)) return NULL;
@@ -1487,6 +1500,7 @@ static napi_value init(napi_env env, napi_value exports) {
         M("lweDecrypt", ctx_lwe_dec),
         {"synchronize", NULL, ctx_synchronize, NULL, NULL, NULL, napi_default, NULL},
         {"info", NULL, ctx_info, NULL, NULL, NULL, napi_default, NULL},
+        {"brRepairCount", NULL, ctx_br_repairs, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_value ctx_cls;
     NAPI_CALL(env, napi_define_class(env, "NttContext", NAPI_AUTO_LENGTH, ctx_ctor, NULL,

@@ -111,6 +111,7 @@ if (mode === 'cpu') {
       else {
         got = U(c.acc);
         e.blindRotate(got, U(c.lwe_a), U([c.lwe_b]), U(c.bsk), c.base_log, c.level);
+        assert.strictEqual(typeof e.brRepairCount(), 'number');
       }
       assert.deepStrictEqual(Array.from(got), c.out.map(BigInt), `${c.op} n=${c.n}`);
     }
