@@ -223,12 +223,28 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 #ifndef FHE_CTMUL_E16
 #define FHE_CTMUL_E16 0
 #endif
+// lab: X0 / Y0 kept in VGPRs instead of the HBM stash (one workgroup per CU):
+// 1 = 32 per thread at a 256-VGPR budget (8 waves; 203 VGPRs), 2 = 16 per
+// thread (16 waves; 99 VGPRs).  Both spill-free and 56 B per coefficient, and
+// both slower than the stash at two workgroups per CU: 4.71 / 4.77 vs 4.59 ms
+// per 16,384 ciphertext pairs (round 5, profiles/r5_ab).  The traffic of the
+// stash (16 B per coefficient) costs less than the lost second workgroup.
+#ifndef FHE_CTMUL_NOSTASH
+#define FHE_CTMUL_NOSTASH 0
+#endif
+template <int LOGN, typename W>
+constexpr bool ctmul_regstash() { return FHE_CTMUL_NOSTASH != 0 && sizeof(W) == 4; }
+template <int LOGN, typename W>
+constexpr int ctmul2_occ() {
+    return ctmul_regstash<LOGN, W>() ? (Geo<LOGN>::THREADS / 64 + 3) / 4 : Geo<LOGN>::template occ_waves<W>();
+}
 template <int LOGN, typename W, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (ctmul2_occ<LOGN, W>()))
 k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_t *out, size_t batch,
           NttArgs<W> A) {
     using G = Geo<LOGN>;
-    static_assert(G::P == 1 && (G::LOGE == 5 || sizeof(W) == 8), "one ciphertext pair per workgroup");
+    constexpr bool RS = ctmul_regstash<LOGN, W>();
+    static_assert(G::P == 1 && (G::LOGE == 5 || sizeof(W) == 8 || RS), "one ciphertext pair per workgroup");
     constexpr int PF = sizeof(W) == 8 ? 0 : 1;  // u64: two 16-word spectra leave no VGPRs for lookahead
     __shared__ W lds[G::LW];
     const uint32_t tau = threadIdx.x;
@@ -237,6 +253,7 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     const uint64_t *xr = x + poly * 2 * G::N, *yr = y + poly * 2 * G::N;
     uint64_t *orow = out + poly * 3 * G::N;
     W *s1 = reinterpret_cast<W *>(orow + G::N), *s2 = reinterpret_cast<W *>(orow + 2 * G::N);
+    W r1[RS ? G::E : 1], r2[RS ? G::E : 1];
     W a[G::E], b[G::E];
     // 1-2
     fwd_poly2<LOGN, LAZY, PF>(lds, a, b, tau, xr, yr, A);
@@ -244,8 +261,13 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(tau, e);
         const W x0 = fwd_to_canon<LAZY>(a[e], A);
-        s1[gi] = x0;
-        s2[gi] = fwd_to_canon<LAZY>(b[e], A);
+        if constexpr (RS) {
+            r1[e] = x0;
+            r2[e] = fwd_to_canon<LAZY>(b[e], A);
+        } else {
+            s1[gi] = x0;
+            s2[gi] = fwd_to_canon<LAZY>(b[e], A);
+        }
         a[e] = A.ar.mont(x0, b[e]);
     }
     __syncthreads();
@@ -261,7 +283,8 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     for (int e = 0; e < G::E; ++e) {
         const uint32_t gi = gidx<LOGN, G::NP - 1>(t2, e);
         const W x1 = fwd_to_canon<LAZY>(a[e], A);
-        const W c1 = A.ar.red2q(A.ar.mont(s1[gi], b[e]) + A.ar.mont(x1, s2[gi]));
+        const W X0 = RS ? r1[RS ? e : 0] : s1[gi], Y0 = RS ? r2[RS ? e : 0] : s2[gi];
+        const W c1 = A.ar.red2q(A.ar.mont(X0, b[e]) + A.ar.mont(x1, Y0));
         b[e] = A.ar.mont(x1, b[e]);
         a[e] = c1;
         // u64: 4 stash pairs in flight at a time (all 16 hoisted spill)
@@ -283,7 +306,7 @@ static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *
     if constexpr ((sizeof(W) == 4 && (LOGN == 13 || LOGN == 14) && !FHE_CTMUL_E16) || (sizeof(W) == 8 && LOGN == 14)) {
         // u64 at N = 16384: 16 coefficients per thread, the pairs in lockstep
         // (no third slot in VGPRs: the single-transform kernel spilled there)
-        constexpr int K = sizeof(W) == 4 ? gk(LOGN, 5) : LOGN;
+        constexpr int K = sizeof(W) == 4 ? gk(LOGN, FHE_CTMUL_NOSTASH == 2 ? 4 : 5) : LOGN;
         if constexpr (sizeof(W) == 4) {
             if (lazy) {
                 hipLaunchKernelGGL((k_ct_mul2<K, W, true>), dim3(batch), dim3(Geo<K>::THREADS), 0, p.stream, x, y,
