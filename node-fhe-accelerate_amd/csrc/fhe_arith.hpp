@@ -367,6 +367,19 @@ struct Arith {
         x = a + b;
         y = sub2q(a, b);
     }
+    // Butterflies with twiddle 1 (compat mode, ntt_core.hpp gk_cp): inputs
+    // in [0, 4q) (forward) / [0, 2q) (inverse), outputs in the same ranges as
+    // ct / gs.
+    __device__ __forceinline__ void ct_unit(W &x, W &y) const {
+        const W a = red2q(x), b = red2q(y);
+        x = a + b;
+        y = sub2q(a, b);
+    }
+    __device__ __forceinline__ void gs_unit(W &x, W &y) const {
+        const W s = x + y, d = sub2q(x, y);
+        x = red2q(s);
+        y = red2q(d);
+    }
     // Gentleman-Sande butterfly, values in [0, 2q).
     template <int SP = 0>
     __device__ __forceinline__ void gs(W &x, W &y, Tw<W> t) const {

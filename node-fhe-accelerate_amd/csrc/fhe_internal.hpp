@@ -37,6 +37,7 @@ struct Plan {
     int word;   // 32 or 64
     int wide;   // q >= 2^62: every transform takes ntt_wide.hip
     int lazy;   // 32-bit path with (4 + 2L) q <= 2^32: forward stages skip reductions
+    int compat; // compat-mode tables (unit twiddle in pass 0): hot kernels take gk_compat keys
     int cus;    // compute units of the context's device (persistent grids)
     hipStream_t stream;
     // N > 2^kMaxFusedLogN (ntt_big.hip): two chunk-sized scratch buffers

@@ -333,7 +333,7 @@ constexpr uint32_t kBrAbort = 0x80000000u;
 #define FHE_BR_PAIR_LOGE_SMALL 2
 #endif
 template <int LOGN>
-constexpr int br_pair_key() { return gk(LOGN, LOGN >= 12 ? FHE_BR_PAIR_LOGE : FHE_BR_PAIR_LOGE_SMALL); }
+constexpr int br_pair_key() { return gk(LOGN, gk_logn(LOGN) >= 12 ? FHE_BR_PAIR_LOGE : FHE_BR_PAIR_LOGE_SMALL); }
 // Levels transformed in lockstep: up to 4, as many LDS exchange regions as
 // fit beside the accumulator (tfhe-256-secure, N = 4096 with 64-bit words:
 // 3 = its whole L).  Levels beyond LB run in further chunks of LB.
@@ -869,6 +869,18 @@ static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, 
 template <typename W>
 static hipError_t br_pair_dispatch(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch,
                                    const NttArgs<W> &A, bool coop) {
+    // 64-bit words in compat mode (the TFHE presets' moduli): unit twiddles
+    // in pass 0 (ntt_core.hpp gk_compat)
+    if constexpr (sizeof(W) == 8) {
+        if (p.compat) {
+            switch (p.logn) {
+            case 10: return br_pair_one<gk_compat(10), W>(p, D, X, batch, A, coop);
+            case 11: return br_pair_one<gk_compat(11), W>(p, D, X, batch, A, coop);
+            case 12: return br_pair_one<gk_compat(12), W>(p, D, X, batch, A, coop);
+            default: return hipErrorInvalidValue;
+            }
+        }
+    }
     switch (p.logn) {
     case 10: return br_pair_one<10, W>(p, D, X, batch, A, coop);
     case 11: return br_pair_one<11, W>(p, D, X, batch, A, coop);

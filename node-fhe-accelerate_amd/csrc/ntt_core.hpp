@@ -51,6 +51,14 @@ constexpr int gk_loge(int k) { return ((k >> 8) & 0xf) ? ((k >> 8) & 0xf) : ((k 
 // key leaves the bits clear.
 constexpr int gk_sparse(int k, int sel) { return k | (sel << 12); }
 constexpr int gk_sp(int k) { return (k >> 12) & 3; }
+// Bit 14: the context is in compat mode (the reference's cyclic transform,
+// whose stage-s twiddle of butterfly 0 is psi^0 = 1).  In pass 0 the twiddle
+// slot of butterfly group 0 is that 1 for every lane, so those butterflies
+// skip the Shoup product (one reduction instead of three multiplies):
+// 31 of the 80 pass-0 butterflies at 32 coefficients per thread, 15 of 32 at
+// 16.  Negacyclic tables have no unit twiddle; their keys leave the bit clear.
+constexpr int gk_compat(int k) { return k | (1 << 14); }
+constexpr bool gk_cp(int k) { return (k >> 14) & 1; }
 
 // Pads for 32 coefficients per thread (tools/lab/lds_pads.py): i + (i >> (L-5))
 // is conflict-free for every pass layout at L = 11..14.
@@ -352,7 +360,11 @@ __device__ __forceinline__ void fwd_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)
         for (int tt = 0; tt < (1 << R); ++tt) {
             if (tt & (1 << K)) continue;
             const int e = tt + (u << R), e2 = e + (1 << K);
+            // unit twiddle (gk_cp): pass 0, butterfly group 0; a lazy stage
+            // above 0 keeps the Shoup form (its inputs exceed 4q)
+            constexpr bool UNIT = gk_cp(LOGN) && PASS == 0 && (!LAZY || K == 0);
             if constexpr (RS && PASS == 0 && K == 0) ar.template ct_rscale<gk_sp(LOGN)>(v[e], v[e2], rmod);
+            else if (UNIT && (tt & ((1 << K) - 1)) == 0) ar.ct_unit(v[e], v[e2]);
             else {
                 const Tw<W> w = t[P::slot(K, u, tt & ((1 << K) - 1))];
                 if constexpr (LAZY) ar.template ct_lazy<gk_sp(LOGN)>(v[e], v[e2], w);
@@ -372,6 +384,7 @@ __device__ __forceinline__ void inv_stage(W (&v)[Geo<LOGN>::E], const Tw<W> (&t)
             if (tt & (1 << K)) continue;
             const int e = tt + (u << R), e2 = e + (1 << K);
             if constexpr (FOLD && S + K == 0) ar.template gs_scaled<gk_sp(LOGN)>(v[e], v[e2], scale);
+            else if (gk_cp(LOGN) && PASS == 0 && (tt & ((1 << K) - 1)) == 0) ar.gs_unit(v[e], v[e2]);
             else ar.template gs<gk_sp(LOGN)>(v[e], v[e2], t[P::slot(K, u, tt & ((1 << K) - 1))]);
         }
 }

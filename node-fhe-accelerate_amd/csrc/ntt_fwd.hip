@@ -198,6 +198,8 @@ static hipError_t fwd_one(const NttArgs<W> &A, hipStream_t s, const uint64_t *in
     constexpr int LOGN = fwd_key<LOGN0, W>();
     using G = Geo<LOGN>;
     const size_t blocks = (batch + G::P - 1) / G::P;
+    // (unit twiddles, ntt_core.hpp gk_compat: 7.29 vs 7.30 ms for the q62 C3
+    // kernel, round 5 -- not instantiated)
     if (wv)
         hipLaunchKernelGGL((k_ntt_fwd_mul<LOGN, W, LAZY>), dim3(blocks), dim3(G::THREADS), 0, s, in, wv, out,
                            batch, A);

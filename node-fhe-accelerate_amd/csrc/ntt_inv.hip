@@ -319,6 +319,8 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
     size_t pblocks = (batch + GP::P - 1) / GP::P;
     if constexpr (polymul_dual<PK, W>()) {
         if (b) {
+            // (unit twiddles, gk_compat, at 32-bit words: 141 fewer multiplies
+            // per wave, 6.32 vs 6.34 ms -- within noise; not instantiated)
             if constexpr (sizeof(W) == 4) {
                 if (lazy)
                     return go(k_polymul2<PK, W, true>, k_polymul2_limbs<PK, W, true>, pblocks, GP::THREADS, a, b, c,
@@ -327,13 +329,21 @@ static hipError_t inv_one(const Plan &p, const NttArgs<W> &A, hipStream_t s, con
             // a sparse prime (ntt_core.hpp gk_sparse): q62 polymul 19.2 -> 18.1 ms
             // per 65,536 (round 5; the forward, the inverse, the multi-level
             // external product and the blind rotation measured 0 to +2 % and
-            // keep the generic arithmetic)
+            // keep the generic arithmetic); compat mode (gk_compat, unit
+            // twiddles in pass 0): 18.39 -> 17.70 ms, 333 fewer multiplies per
+            // wave, and no spill
             if constexpr (sizeof(W) == 8) {
+                if (!tab && A.ar.sp == 1 && p.compat)
+                    return go(k_polymul2<gk_compat(gk_sparse(PK, 1)), W, false>, k_polymul2_limbs<PK, W, false>,
+                              pblocks, GP::THREADS, a, b, c, batch);
                 if (!tab && A.ar.sp == 1)
                     return go(k_polymul2<gk_sparse(PK, 1), W, false>, k_polymul2_limbs<PK, W, false>, pblocks,
                               GP::THREADS, a, b, c, batch);
                 if (!tab && A.ar.sp == 2)
                     return go(k_polymul2<gk_sparse(PK, 2), W, false>, k_polymul2_limbs<PK, W, false>, pblocks,
+                              GP::THREADS, a, b, c, batch);
+                if (!tab && p.compat)
+                    return go(k_polymul2<gk_compat(PK), W, false>, k_polymul2_limbs<PK, W, false>, pblocks,
                               GP::THREADS, a, b, c, batch);
             }
             return go(k_polymul2<PK, W, false>, k_polymul2_limbs<PK, W, false>, pblocks, GP::THREADS, a, b, c, batch);

@@ -509,3 +509,29 @@ def test_dense_62bit_prime_vs_oracle(fg):
     assert (r.forward_ntt_mul(x, y) == t.fwd_mul(x, y)).all()
     assert (r.multiply(x, y) == t.polymul(x, y)).all()
     assert (r.inverse_ntt(x) == t.inverse(x)).all()
+
+
+@pytest.mark.parametrize("q", [P62, Q_DENSE62])
+def test_unit_twiddle_kernels_match_generic(fg, monkeypatch, q):
+    """Compat-mode contexts take unit-twiddle kernels for the 64-bit polymul
+    (ntt_core.hpp gk_compat: pass-0 butterflies of group 0 skip the Shoup
+    product); FHE_UNIT_TW=0 at context creation keeps the generic ones.  Both
+    agree word for word (raw input words included), negacyclic contexts never
+    take them, and rows match the oracle."""
+    n, b = 16384, 4
+    x, y = rnd(521, q, b, n), rnd(522, q, b, n)
+    x[0, :3] = [2**64 - 1, q, q + 1]
+    out = {}
+    for u in ("0", "1"):
+        monkeypatch.setenv("FHE_UNIT_TW", u)
+        out[u] = fg.PolynomialRing(n, q).multiply(x, y)
+    assert (out["0"] == out["1"]).all()
+    t = oracle.NTT(n, q)
+    assert (out["1"][[0, b - 1]] == t.polymul(x[[0, b - 1]], y[[0, b - 1]])).all()
+    # negacyclic context (no unit twiddle): x * X is the signed shift
+    monkeypatch.setenv("FHE_UNIT_TW", "1")
+    X = np.zeros((1, n), np.uint64)
+    X[0, 1] = 1
+    expect = np.roll(x[1:2], 1, axis=1)
+    expect[0, 0] = (q - int(x[1, -1])) % q
+    assert (fg.PolynomialRing(n, q, mode="negacyclic").multiply(x[1:2], X) == expect).all()
