@@ -556,8 +556,9 @@ BENCH_KERNELS = {
     "fwd_mul/q27": "void fhe::k_ntt_fwd_mul<14, unsigned int, true>" + _nargs("int"),
     "polymul/q27": "void fhe::k_polymul2<1294, unsigned int, true>" + _nargs("int"),
     "fwd_mul/q62": "void fhe::k_ntt_fwd_mul<1294, unsigned long, false>" + _nargs("long"),
-    # the 62-bit prime takes the prime-specialised kernels (key bit 12: gk_sparse(14, 1) = 4110)
-    "polymul/q62": "void fhe::k_polymul2<4110, unsigned long, false>" + _nargs("long"),
+    # the 62-bit prime takes the prime-specialised kernels (key bit 12: gk_sparse(14, 1) = 4110),
+    # the compat-mode polymul also the unit-twiddle form (bit 14: gk_compat(4110) = 20494)
+    "polymul/q62": "void fhe::k_polymul2<20494, unsigned long, false>" + _nargs("long"),
     "extprod_B23_L1": "void fhe::k_extprod2<4110, unsigned long>(fhe::DmArgs, fhe::NttArgs<unsigned long>)",
     "extprod_B15_L2": "void fhe::k_extprod_acc<1294>(fhe::ExtAccArgs, fhe::NttArgs<unsigned long>)",
     "ct_multiply": "void fhe::k_ct_mul2<1294, unsigned int, true>" + _nargs("int"),
