@@ -71,9 +71,9 @@ struct BrArgs {
 #define FHE_BR_LOGE_SMALL FHE_BR_LOGE
 #endif
 template <int LOGN>
-constexpr int br_key() {
-    return LOGN >= 12 ? gk(LOGN, FHE_BR_LOGE)
-                      : gk(LOGN, LOGN - 7 < FHE_BR_LOGE_SMALL ? LOGN - 7 : FHE_BR_LOGE_SMALL);
+constexpr int br_key() {  // LOGN may carry key bits (gk_compat)
+    constexpr int L = gk_logn(LOGN);
+    return L >= 12 ? gk(LOGN, FHE_BR_LOGE) : gk(LOGN, L - 7 < FHE_BR_LOGE_SMALL ? L - 7 : FHE_BR_LOGE_SMALL);
 }
 template <int LOGN>
 constexpr int br_threads() { return 2 * Geo<br_key<LOGN>()>::T; }
@@ -804,6 +804,24 @@ static hipError_t br_one(const Plan &p, int k1, const BrArgs &D, size_t batch, c
 }
 template <typename W>
 static hipError_t br_dispatch(const Plan &p, int k1, const BrArgs &D, size_t batch, const NttArgs<W> &A) {
+    // k = 1 with 64-bit words in compat mode: unit twiddles in pass 0
+    // (ntt_core.hpp gk_compat), as in the two-CU kernel
+    if constexpr (sizeof(W) == 8) {
+        if (p.compat && k1 == 2 && p.logn >= 10) {
+            const auto go = [&](auto K) -> hipError_t {
+                constexpr int L = decltype(K)::value;
+                hipLaunchKernelGGL((k_br_persist<L, W>), dim3((unsigned)batch), dim3(br_threads<L>()), 0, p.stream,
+                                   D, A);
+                return hipGetLastError();
+            };
+            switch (p.logn) {
+            case 10: return go(std::integral_constant<int, gk_compat(10)>{});
+            case 11: return go(std::integral_constant<int, gk_compat(11)>{});
+            case 12: return go(std::integral_constant<int, gk_compat(12)>{});
+            default: break;
+            }
+        }
+    }
     switch (p.logn) {
     case 9: return br_one<9, W>(p, k1, D, batch, A);
     case 10: return br_one<10, W>(p, k1, D, batch, A);
