@@ -275,6 +275,32 @@ def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop):
     assert (acc == ref).all() and be.repair_count() == before
 
 
+@pytest.mark.parametrize("b", [37, 100])
+def test_br_pair_ragged_batches(fg, monkeypatch, b):
+    """Batches that fill the two-CU grid (16 workgroups per 8 ciphertexts,
+    ct = (block >> 4) * 8 + (block & 7)) only partly: the workgroups past the
+    batch leave at once and every ciphertext equals the one-CU kernel's, rows
+    0 and b - 1 the oracle's (tfhe-128-balanced shape, compat mode: the
+    unit-twiddle kernels)."""
+    n, q, bl, lv, k, dim = 2048, Q50, 15, 2, 1, 6
+    r = fg.PolynomialRing(n, q)
+    be = fg.BootstrapEngine(r, bl, lv, k)
+    bsk = rnd(191, q, dim, (k + 1) * lv, k + 1, n)
+    bsk_ntt = be.prepare_ggsw(bsk)
+    lwe_a, lwe_b = rnd(192, q, b, dim), rnd(193, q, b)
+    acc0 = rnd(194, q, b, k + 1, n)
+    got = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("FHE_BR_PAIR", pair)
+        acc = acc0.copy()
+        be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
+        got[pair] = acc
+    assert (got["1"] == got["0"]).all()
+    t = oracle.NTT(n, q)
+    for i in (0, b - 1):
+        assert (got["1"][i] == t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])).all(), i
+
+
 @pytest.mark.parametrize("serial", ["1", "0"])
 def test_br_pair_concurrent_contexts(fg, monkeypatch, serial):
     """Two contexts run two-CU blind rotations on two streams at once, with
