@@ -127,11 +127,18 @@ constexpr int polymul_pf() { return Geo<LOGN>::LOGE == 5 ? FHE_PF_POLY32 : kPfPo
 #ifndef FHE_PF_DUAL64
 #define FHE_PF_DUAL64 0
 #endif
+// The dual kernel also at N = 4096 with 16 per thread (one 256-thread
+// workgroup per pair, <= 128 VGPRs): 30.3 -> 28.1 us for C2's 1024 pairs,
+// 1.67 -> 1.49 ms (q < 2^27, lazy) and 1.74 -> 1.62 ms (q < 2^30) per 65,536
+// (round 5).  FHE_POLY_DUAL_E16=0 keeps the single-transform kernel.
+#ifndef FHE_POLY_DUAL_E16
+#define FHE_POLY_DUAL_E16 1
+#endif
 template <int LOGN, typename W>
 constexpr bool polymul_dual() {
     using G = Geo<LOGN>;
     if constexpr (sizeof(W) == 4)
-        return G::LOGE == 5 && FHE_POLY_DUAL;
+        return (G::LOGE == 5 && FHE_POLY_DUAL) || (FHE_POLY_DUAL_E16 && G::P == 1 && G::LOGE == 4 && G::L == 12);
     else return FHE_POLY_DUAL64 && G::P == 1 && G::L == 14 && G::LOGE == 4 && FHE_POLY64 == 1;
 }
 template <int LOGN, typename W>
@@ -237,8 +244,13 @@ __device__ __forceinline__ void polymul2_one(W *lds, uint32_t tau, const uint64_
     inv_poly_from_regs<LOGN, polymul2_pf<LOGN, W>()>(lds, v, tau, c + poly * G::N, true, A, A.ninv_r);
 }
 
+template <int LOGN, typename W>
+constexpr int polymul2_occ() {
+    constexpr int o = Geo<LOGN>::template occ_waves<W>();
+    return (FHE_POLY_DUAL_E16 && Geo<LOGN>::LOGE == 4 && sizeof(W) == 4 && o > 4) ? 4 : o;
+}
 template <int LOGN, typename W, bool LAZY>
-__global__ void __launch_bounds__(Geo<LOGN>::THREADS, Geo<LOGN>::template occ_waves<W>())
+__global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul2_occ<LOGN, W>()))
 k_polymul2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t *c, size_t batch,
            NttArgs<W> A) {
     using G = Geo<LOGN>;
