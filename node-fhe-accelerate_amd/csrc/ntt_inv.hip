@@ -127,6 +127,13 @@ constexpr int polymul_pf() { return Geo<LOGN>::LOGE == 5 ? FHE_PF_POLY32 : kPfPo
 #ifndef FHE_PF_DUAL64
 #define FHE_PF_DUAL64 0
 #endif
+// The 64-bit dual kernel also at N = 4096 / 8192 (16 per thread, one
+// workgroup per pair, occupancy floor 4 waves per SIMD; 123-126 VGPRs, no
+// spill): per 16,384 pairs at N = 8192 2.83 -> 2.23 ms (Q_60_1) and 2.75 ->
+// 2.10 ms (the 62-bit prime), at N = 4096 1.23 -> 1.06 ms (Q_60_1) (round 5).
+#ifndef FHE_POLY_DUAL64_SMALL
+#define FHE_POLY_DUAL64_SMALL 1
+#endif
 // The dual kernel also at N = 4096 with 16 per thread (one 256-thread
 // workgroup per pair, <= 128 VGPRs): 30.3 -> 28.1 us for C2's 1024 pairs,
 // 1.67 -> 1.49 ms (q < 2^27, lazy) and 1.74 -> 1.62 ms (q < 2^30) per 65,536
@@ -139,7 +146,8 @@ constexpr bool polymul_dual() {
     using G = Geo<LOGN>;
     if constexpr (sizeof(W) == 4)
         return (G::LOGE == 5 && FHE_POLY_DUAL) || (FHE_POLY_DUAL_E16 && G::P == 1 && G::LOGE == 4 && G::L == 12);
-    else return FHE_POLY_DUAL64 && G::P == 1 && G::L == 14 && G::LOGE == 4 && FHE_POLY64 == 1;
+    else return FHE_POLY_DUAL64 && G::P == 1 && G::LOGE == 4 &&
+                ((G::L == 14 && FHE_POLY64 == 1) || (FHE_POLY_DUAL64_SMALL && (G::L == 12 || G::L == 13)));
 }
 template <int LOGN, typename W>
 constexpr int polymul2_pf() { return sizeof(W) == 8 ? FHE_PF_DUAL64 : polymul_pf<LOGN>(); }
@@ -247,7 +255,7 @@ __device__ __forceinline__ void polymul2_one(W *lds, uint32_t tau, const uint64_
 template <int LOGN, typename W>
 constexpr int polymul2_occ() {
     constexpr int o = Geo<LOGN>::template occ_waves<W>();
-    return (FHE_POLY_DUAL_E16 && Geo<LOGN>::LOGE == 4 && sizeof(W) == 4 && o > 4) ? 4 : o;
+    return (FHE_POLY_DUAL_E16 && Geo<LOGN>::LOGE == 4 && (sizeof(W) == 4 || gk_logn(LOGN) < 14) && o > 4) ? 4 : o;
 }
 template <int LOGN, typename W, bool LAZY>
 __global__ void __launch_bounds__(Geo<LOGN>::THREADS, (polymul2_occ<LOGN, W>()))

@@ -83,7 +83,11 @@ CONFIGS = [(4, 17), (8, 17), (16, 97), (32, 193), (64, 257), (128, 769), (256, 7
            (32768, P27), (32768, P62), (65536, P27), (65536, P62),
            # q in (2^27, 2^30): 32-bit lanes without the lazy forward (the
            # 32-coefficient polymul's non-lazy instantiation at N=8192/16384)
-           (8192, 1073643521), (16384, 1073643521)]
+           (8192, 1073643521), (16384, 1073643521),
+           # the paired-transform polymul at N = 4096 / 8192 (round 5): 32-bit
+           # non-lazy, Q_60_1 (prime-specialised), a dense 62-bit prime (generic)
+           (4096, 1073643521), (4096, 1152921504606584833), (8192, 1152921504606584833),
+           (4096, 3458764513825652737), (8192, 3458764513825652737)]
 
 
 @pytest.mark.parametrize("n,q", CONFIGS)
