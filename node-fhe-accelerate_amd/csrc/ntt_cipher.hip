@@ -223,6 +223,13 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 #ifndef FHE_CTMUL_E16
 #define FHE_CTMUL_E16 0
 #endif
+// The paired kernel also for 64-bit words at N = 4096 / 8192 (instead of the
+// slot kernel): per 16,384 ciphertext pairs at N = 8192 1.80 -> 1.55 ms
+// (Q_60_1) and 1.73 -> 1.50 ms (62-bit prime), at N = 4096 0.80 -> 0.75 ms
+// (round 5).
+#ifndef FHE_CTMUL2_U64_SMALL
+#define FHE_CTMUL2_U64_SMALL 1
+#endif
 // lab: X0 / Y0 kept in VGPRs instead of the HBM stash (one workgroup per CU):
 // 1 = 32 per thread at a 256-VGPR budget (8 waves; 203 VGPRs), 2 = 16 per
 // thread (16 waves; 99 VGPRs).  Both spill-free and 56 B per coefficient, and
@@ -303,7 +310,8 @@ static hipError_t ctmul_one(const Plan &p, const NttArgs<W> &A, const uint64_t *
     const size_t blocks = (batch + G::P - 1) / G::P;
     bool lazy = false;
     if constexpr (sizeof(W) == 4) lazy = p.lazy;
-    if constexpr ((sizeof(W) == 4 && (LOGN == 13 || LOGN == 14) && !FHE_CTMUL_E16) || (sizeof(W) == 8 && LOGN == 14)) {
+    if constexpr ((sizeof(W) == 4 && (LOGN == 13 || LOGN == 14) && !FHE_CTMUL_E16) ||
+                  (sizeof(W) == 8 && (LOGN == 14 || (FHE_CTMUL2_U64_SMALL && (LOGN == 12 || LOGN == 13))))) {
         // u64 at N = 16384: 16 coefficients per thread, the pairs in lockstep
         // (no third slot in VGPRs: the single-transform kernel spilled there)
         constexpr int K = sizeof(W) == 4 ? gk(LOGN, FHE_CTMUL_NOSTASH == 2 ? 4 : 5) : LOGN;

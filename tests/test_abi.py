@@ -181,6 +181,11 @@ SCRATCH_EXEMPT = {
     # 29.6 ms vs 31.0 ms one level at a time
     "k_br_pair<12, unsigned long, 3>",
     "k_br_pair<16396, unsigned long, 3>",  # the same kernel with unit twiddles (gk_compat(12))
+    # the paired 64-bit ciphertext multiply at N = 4096 / 8192: 3 VGPRs spilled
+    # (as its N = 16384 instantiation), 13-14 % faster than the scratch-free
+    # slot kernel
+    "k_ct_mul2<12, unsigned long, false>",
+    "k_ct_mul2<13, unsigned long, false>",
 }
 # Ratchet: kernels that still use scratch anywhere (small-degree u64 digit
 # kernels, the ciphertext-multiply stash); the count may only go down (95 in

@@ -33,11 +33,12 @@ def rnd(seed, q, *shape):
 
 
 # ------------------------------------------------------------ ciphertext multiply
-# (4096, P62) and (8192, P27) take the VGPR-slot layout (FHE_CTMUL_PREFER_REGS)
+# (4096, P27) takes the VGPR-slot layout (FHE_CTMUL_PREFER_REGS); 64-bit words
+# at N = 4096 / 8192 / 16384 the paired kernel (round 5: also Q_60_1 at 8192)
 # (8192 / 16384, 1073643521): the non-lazy 32-bit paired kernel (q in (2^27, 2^30))
 @pytest.mark.parametrize("n,q", [(4, 17), (16, 97), (256, 7681), (1024, P27), (2048, P62), (4096, P27),
                                  (4096, P62), (8192, P27), (8192, P62), (16384, P27), (16384, P62),
-                                 (8192, 1073643521), (16384, 1073643521)])
+                                 (8192, 1073643521), (16384, 1073643521), (8192, 1152921504606584833)])
 def test_ct_multiply_vs_oracle(fg, n, q):
     b = 3 if n >= 8192 else 5
     r = fg.PolynomialRing(n, q)
