@@ -307,7 +307,7 @@ def negacyclic_workload(fhe_gpu, n, q, batch, steps, warmup, dist):
         ach = 24 * n * batch / (kms * 1e-3) / 1e9
         out[key] = {"per_s": batch * steps / wall, "kernel_ms": kms, "achieved_GBs": ach,
                     "frac": ach / HBM_PEAK_GBS, "bytes_per_unit": 24 * n}
-        _attach(out[key], pmc_traffic(key, n, batch, q, mode="negacyclic"), 24 * n * batch)
+        _attach(out[key], pmc_traffic(key, n, batch, q, mode="negacyclic"), 24 * n * batch, kms)
     return out
 
 
@@ -406,7 +406,7 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
                                   "transforms_per_unit": 7, "bytes_per_unit": 56 * n,
                                   "achieved_GBs": 56 * n * B / (kms * 1e-3) / 1e9}
             _attach(res["ct_multiply"], profile_traffic("ct_multiply", {"kernel": "ct_mul", "n": n, "batch": B, "q": q}),
-                    56 * n * B)
+                    56 * n * B, kms)
         if only in ("", "relin"):
             ek = fhe_gpu.EvaluationKey(ring, torch.randint(0, q, (lv, 2, n), device="cuda", dtype=torch.int64,
                                                            generator=g), bl)
@@ -417,7 +417,7 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
                                   "kernel_ms": kms, "transforms_per_unit": lv + 2, "bytes_per_unit": 40 * n,
                                   "achieved_GBs": 40 * n * B / (kms * 1e-3) / 1e9}
             _attach(res["relinearize"], profile_traffic("relinearize", {"kernel": "relin", "n": n, "batch": B, "q": q}),
-                    40 * n * B)
+                    40 * n * B, kms)
             del out, ek
         del x, y, ct3
     if only in ("", "c5"):
@@ -438,7 +438,7 @@ def cipher_workload(fhe_gpu, steps, warmup, dist, only=""):
                                           "transforms_per_unit": 2 * lv + 2,
                                           "algorithmic_bytes_per_launch": alg,
                                           "achieved_GBs": alg / (kms * 1e-3) / 1e9}
-            _attach(c5[f"extprod_B{bl}_L{lv}"], profile_traffic(f"extprod_B{bl}_L{lv}"), alg)
+            _attach(c5[f"extprod_B{bl}_L{lv}"], profile_traffic(f"extprod_B{bl}_L{lv}"), alg, kms)
         del glwe, out
         cnt = 16384 * 1024
         ml = fhe_gpu.MultiLimbModularArithmetic([0xFFFFFFFF00000001, 0x3FFFFFFFFFFFFFFF])
@@ -528,6 +528,13 @@ def br_presets(fhe_gpu, dist, g, batches=(1, 64, 8192)):
             reps = 3 if b <= 64 else 1
             wall, kms = timed(dist, lambda: be.blind_rotate(acc, la, lb, bsk), reps, 1)
             rec[f"batch{b}"] = {"ms": kms, "per_s": b * reps / wall, "ms_per_bootstrap_at_batch": kms / b}
+            if b == 64 and name == "tfhe-256-secure":
+                # unique bytes of one launch: the bootstrapping key once, the
+                # accumulators in and out, the LWE masks
+                alg = dim * 2 * lv * 2 * n * 8 + 2 * b * 2 * n * 8 + b * (dim + 1) * 8
+                rec[f"batch{b}"]["algorithmic_bytes_per_launch"] = alg
+                _attach(rec[f"batch{b}"], profile_traffic("br_pair/tfhe-256-secure",
+                                                          {"kernel": "br_pair", "n": n, "batch": b, "q": q}), alg, kms)
             wall, kms = timed(dist, lambda: be.bootstrap(la, lb, bsk, tp, ksk_a, ksk_b, bl, lv), reps, 1)
             boot[f"batch{b}"] = {"ms": kms, "per_s": b * reps / wall}
             ea = torch.randint(0, q, (b, n), device="cuda", dtype=torch.int64, generator=g)
@@ -563,6 +570,10 @@ BENCH_KERNELS = {
     "extprod_B15_L2": "void fhe::k_extprod_acc<1294>(fhe::ExtAccArgs, fhe::NttArgs<unsigned long>)",
     "ct_multiply": "void fhe::k_ct_mul2<1294, unsigned int, true>" + _nargs("int"),
     "relinearize": "void fhe::k_dmac<14, unsigned int, 2, false, 1>(fhe::DmArgs, fhe::NttArgs<unsigned int>)",
+    # tfhe-256-secure blind rotation at batch 64: two CUs per ciphertext, unit
+    # twiddles (gk_compat(12) = 16396), its three digit levels in lockstep
+    "br_pair/tfhe-256-secure": "void fhe::k_br_pair<16396, unsigned long, 3>(fhe::BrArgs, fhe::NttArgs<unsigned long>, "
+                               "fhe::BrPairX, unsigned int)",
 }
 
 
@@ -575,11 +586,11 @@ def _build_id():
         return None
 
 
-def profile_traffic(key, workload=None):
-    """(HBM bytes per launch, summary path, profiled kernel ms) from the
-    newest profiles/*/summary.json of kernel BENCH_KERNELS[key] stamped with
-    the loaded library's build id (and, when given, the same workload), or
-    None.  Written by tools/gpu_evidence.sh + tools/summarize_profile.py."""
+def matched_summary(key, workload=None):
+    """(summary dict, path) of the newest profiles/*/summary.json of kernel
+    BENCH_KERNELS[key] stamped with the loaded library's build id (and, when
+    given, the same workload), or None.  Written by tools/gpu_evidence.sh +
+    tools/summarize_profile.py."""
     import glob
 
     sym, bid = BENCH_KERNELS[key], _build_id()
@@ -600,10 +611,19 @@ def profile_traffic(key, workload=None):
                 continue
         key_ = (s.get("generated", ""), f)
         if best is None or key_ > best[0]:
-            kt = s.get("kernel_trace_full_batch", {})
-            best = (key_, s["hbm_traffic_bytes_per_launch"], os.path.relpath(f, ROOT),
-                    kt.get("avg_ns", 0) / 1e6 or None)
+            best = (key_, s, os.path.relpath(f, ROOT))
     return best[1:] if best else None
+
+
+def profile_traffic(key, workload=None):
+    """(HBM bytes per launch, summary path, profiled kernel ms, summary) of
+    matched_summary(), or None."""
+    m = matched_summary(key, workload)
+    if m is None:
+        return None
+    s, path = m
+    kt = s.get("kernel_trace_full_batch", {})
+    return s["hbm_traffic_bytes_per_launch"], path, kt.get("avg_ns", 0) / 1e6 or None, s
 
 
 def pmc_traffic(kernel, n, batch, q, mode="compat"):
@@ -614,11 +634,25 @@ def pmc_traffic(kernel, n, batch, q, mode="compat"):
     return profile_traffic(key, {"kernel": kernel, "n": n, "batch": batch, "q": q, "mode": mode})
 
 
-def _attach(d, tr, alg):
-    """Traffic fields of a roofline / side-metric record (null when unmatched)."""
+def _attach(d, tr, alg, kernel_ms=None):
+    """Traffic and second-roofline fields of a roofline / side-metric record
+    (traffic null when unmatched).  From the matched profile summary: the
+    HBM fraction priced on the profile's own kernel time beside the
+    event-timed one (`frac_profile`), and the VALU-issue roofline
+    (tools/valu_roofline.py) priced on both times."""
     if tr:
-        d["traffic"], d["traffic_source"], d["profile_kernel_ms"] = tr
+        d["traffic"], d["traffic_source"], d["profile_kernel_ms"] = tr[:3]
         d["traffic_over_algorithmic"] = tr[0] / alg
+        s = tr[3] if len(tr) > 3 else None
+        if s is not None:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import valu_roofline as vr
+
+            fp = vr.hbm_frac_profile(s, alg, HBM_PEAK_GBS)
+            if fp is not None:
+                d["frac_profile"] = fp
+            v = vr.valu_roofline(s, vr.load_rates(), kernel_ms=kernel_ms)
+            d["valu_roofline"] = v if v is not None else "no VALU counters / static mix in the matched profile"
     else:
         d["traffic"] = None
         d["traffic_source"] = "no profile of this exact kernel on this build (fhe_build_id)"
@@ -639,6 +673,33 @@ def host_info():
     except Exception:
         aff = os.cpu_count() or 1
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
+
+
+def cpu_calibration(n, q):
+    """BASELINE.md section 2's calibration of the port against the compiled
+    reference: tools/calibrate_cpu.py times oracle/ref_cpu.c in the survey
+    container class at SURVEY.md section 6's configs (one thread) and divides
+    by the reference timings recorded there (profiles/r6_cpu_calibration.json).
+    ratio > 1: the port is slower than the reference by that factor, so the
+    reference's own throughput would be cpu_baseline.value x ratio."""
+    path = os.path.join(ROOT, "profiles", "r6_cpu_calibration.json")
+    try:
+        cal = json.load(open(path))
+    except (OSError, ValueError):
+        return {"status": "uncalibrated: profiles/r6_cpu_calibration.json missing"}
+    rows = {(r["op"], r["q"], r["n"]): r for r in cal["rows"]}
+    out = {"source": os.path.relpath(path, ROOT), "host": cal.get("host"), "generated": cal.get("generated"),
+           "meaning": "port time / compiled-reference time per call, one thread, same container class "
+                      "(reference: SURVEY.md section 6 [verified] timings; not buildable on the GPU box)",
+           "ratio_median_all_configs": cal["ratio_median"], "ratio_range": [cal["ratio_min"], cal["ratio_max"]]}
+    for op in ("forward_ntt", "multiply"):
+        r = rows.get((op, q, n))
+        if r:
+            out[f"{op}_N{n}"] = {"port_us": r["port_us"], "reference_us": r["reference_us"], "ratio": r["ratio"]}
+    fw = rows.get(("forward_ntt", q, n))
+    if fw:
+        out["within_10pct_at_this_config"] = 0.9 <= fw["ratio"] <= 1.1
+    return out
 
 
 def cpu_baseline(n, q, seconds, threads=None):
@@ -675,8 +736,7 @@ def cpu_baseline(n, q, seconds, threads=None):
     else:
         basis = "every CPU this process may run on"
     return {"value": done / el, "unit": "NTTs/s", "cores": threads, "cores_basis": basis, "kind": "port",
-            "calibration": "uncalibrated port: the reference C++ is not buildable here (modular_arithmetic.h "
-                           "includes <arm_neon.h>), so the +-10% calibration of BASELINE.md section 2 was not possible",
+            "calibration": cpu_calibration(n, q),
             **info,
             "sample": f"{done} x (forward NTT + pointwise modmul), N={n}, q={q}, {threads} threads, {el:.1f}s; "
                       f"oracle/ref_cpu.c restatement of NTTProcessor::forward_ntt + pointwise_multiply"}
@@ -721,7 +781,7 @@ def main():
                                  "frac": achp62 / HBM_PEAK_GBS},
         }
         for key, rl in (("fwd_mul", extra["q62"]["roofline"]), ("polymul", extra["q62"]["polymul_roofline"])):
-            _attach(rl, pmc_traffic(key, n, B, P62), 24 * n * B)
+            _attach(rl, pmc_traffic(key, n, B, P62), 24 * n * B, r62[key][1])
     if not args.only:
         nk = max(3, K // 4)
         extra["negacyclic"] = negacyclic_workload(fhe_gpu, n, args.q, B, nk, 1, dist)
@@ -765,7 +825,7 @@ def main():
         "parity_ok": r["parity_ok"],
         "parity_rows": r.get("parity_rows"),
     }
-    _attach(line["roofline"], pmc_traffic(key, n, B, args.q), bytes_per_unit * B)
+    _attach(line["roofline"], pmc_traffic(key, n, B, args.q), bytes_per_unit * B, kms)
     line["build_id"] = _build_id()
     if "gather" in r:
         line["gather"] = r["gather"]
@@ -773,9 +833,11 @@ def main():
         pw, pk = r["polymul"]
         line["polymuls_per_s"] = world * B * K / pw
         line["polymul_roofline"] = {"achieved": 24 * n * B / (pk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                                    "unit": "GB/s", "kernel_ms": pk,
-                                    "bound": "valu (3 transforms per 24N bytes; DESIGN.md section 6)"}
-        _attach(line["polymul_roofline"], pmc_traffic("polymul", n, B, args.q), 24 * n * B)
+                                    "unit": "GB/s", "kernel_ms": pk, "frac": 24 * n * B / (pk * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "bound": "valu",
+                                    "bound_note": "3 transforms per 24N bytes: the VALU-issue roofline is "
+                                                  "valu_roofline (DESIGN.md section 6)"}
+        _attach(line["polymul_roofline"], pmc_traffic("polymul", n, B, args.q), 24 * n * B, pk)
     line.update(extra)
     if not args.no_cpu and world == 1 and not args.only:
         line["cpu_baseline"] = cpu_baseline(n, args.q, args.cpu_seconds)

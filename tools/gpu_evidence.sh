@@ -21,6 +21,8 @@ OUT=gpurun_out/evidence_$TAG
 mkdir -p $OUT
 echo "build_id $BID" > $OUT/build_id.txt
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT"
+# VALU-issue roofline (tools/valu_roofline.py): busy cycles + the clock
+SQ2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES SQ_INST_LEVEL_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT"
 
 # name -> bench args | summaries (kernel-substr=workload ...)
 spec() {
@@ -33,8 +35,6 @@ spec() {
     nega_polymul) echo "--only polymul --no-check --no-q62 --mode negacyclic|k_polymul=polymul,16384,65536,$P27,negacyclic";;
     ct_mul)       echo "--only ct_mul|k_ct_mul=ct_mul,16384,8192,$P27";;
     relin)        echo "--only relin|k_dmac=relin,16384,8192,$P27";;
-    # (cooperative launch off under the profiler: rocprofv3 7.2 segfaults in
-    # its exit handlers after any hipLaunchCooperativeKernel; same kernel)
     br)           echo "--only br_presets|k_br_pair=br_pair,4096,64,1152921504606584833";;
     c5)           echo "--only c5|k_extprod2=extprod_B23_L1,16384,4096,$P62 k_extprod_acc=extprod_B15_L2,16384,4096,$P62";;
     *) return 1;;
@@ -46,7 +46,6 @@ for wl in $WLS; do
   args=${sp%%|*}; sums=${sp#*|}
   d=$OUT/$wl; mkdir -p $d
   B="bench.py --steps 10 --warmup 3 $args"
-  if [ $wl = br ]; then export FHE_BR_PAIR_COOP=0; else unset FHE_BR_PAIR_COOP; fi
   echo "$wl: trace $(date +%T)" | tee -a $OUT/progress.log
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d/trace -o run --output-format csv -- python3 $B \
     > $d/trace.log 2>&1 || { echo "$wl trace failed rc=$?"; tail -5 $d/trace.log; exit 1; }
@@ -54,7 +53,7 @@ for wl in $WLS; do
   # relinearisation: L2 -> CU read requests and L2 hit/miss (the prepared
   # key is re-read from L2 by every workgroup)
   EXTRA=""; [ $wl = relin ] && EXTRA="TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum"
-  for ctr in FETCH_SIZE WRITE_SIZE "$SQ" ${EXTRA:+"$EXTRA"}; do
+  for ctr in FETCH_SIZE WRITE_SIZE "$SQ" "$SQ2" ${EXTRA:+"$EXTRA"}; do
     i=$((i + 1))
     echo "$wl: pmc$i $(date +%T)" >> $OUT/progress.log
     timeout -s KILL 240 rocprofv3 --pmc $ctr -d $d/pmc_$i -o run --output-format csv -- python3 $B \

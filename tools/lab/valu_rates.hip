@@ -39,6 +39,33 @@ KERNEL(k_mul64, double, (double)SEED32, asm volatile("v_mul_f64 %0, %0, %1" : "+
 KERNEL(k_fma32, float, (float)SEED32, asm volatile("v_fma_f32 %0, %0, %1, %0" : "+v"(v[c]) : "v"((float)seed)))
 KERNEL(k_cvt_f64_u32, double, (double)SEED32, { uint32_t t; asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(t) : "v"(v[c])); asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(v[c]) : "v"(t)); })
 KERNEL(k_cvt_f32_u32, float, (float)SEED32, { uint32_t t; asm volatile("v_cvt_u32_f32 %0, %1" : "=v"(t) : "v"(v[c])); asm volatile("v_cvt_f32_u32 %0, %1" : "=v"(v[c]) : "v"(t)); })
+KERNEL(k_sub, uint32_t, SEED32, asm volatile("v_sub_u32 %0, %0, %1" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_mov, uint32_t, SEED32, asm volatile("v_mov_b32 %0, %1" : "=v"(v[c]) : "v"(v[(c + 1) % CH])))
+KERNEL(k_and, uint32_t, SEED32, asm volatile("v_and_b32 %0, %0, %1" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_lshr, uint32_t, SEED32, asm volatile("v_lshrrev_b32 %0, %1, %0" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_bfi, uint32_t, SEED32, asm volatile("v_bfi_b32 %0, %0, %1, %0" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_lshr64, uint64_t, (uint64_t)SEED32, asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(v[c])))
+KERNEL(k_addco, uint32_t, SEED32, asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(v[c]) : "v"(seed) : "vcc"))
+KERNEL(k_addc, uint32_t, SEED32, asm volatile("v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(v[c]) : "v"(seed) : "vcc"))
+KERNEL(k_cndmask, uint32_t, SEED32, asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[c]) : "v"(seed) : "vcc"))
+KERNEL(k_cmp64, uint64_t, (uint64_t)SEED32, { uint64_t m; asm volatile("v_cmp_lt_u64_e64 %0, %1, %2" : "=s"(m) : "v"(v[c]), "v"((uint64_t)seed)); asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(*(uint32_t *)&v[c]) : "v"(seed), "s"(m)); })
+KERNEL(k_cmp32, uint32_t, SEED32, { uint64_t m; asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m) : "v"(v[c]), "v"(seed)); asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(seed), "s"(m)); })
+KERNEL(k_not, uint32_t, SEED32, asm volatile("v_not_b32 %0, %0" : "+v"(v[c])))
+KERNEL(k_ashr, uint32_t, SEED32, asm volatile("v_ashrrev_i32 %0, %1, %0" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_subrev, uint32_t, SEED32, asm volatile("v_subrev_u32 %0, %0, %1" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_subco, uint32_t, SEED32, asm volatile("v_sub_co_u32 %0, vcc, %0, %1" : "+v"(v[c]) : "v"(seed) : "vcc"))
+KERNEL(k_subb, uint32_t, SEED32, asm volatile("v_subb_co_u32 %0, vcc, %0, %1, vcc" : "+v"(v[c]) : "v"(seed) : "vcc"))
+KERNEL(k_lshl32, uint32_t, SEED32, asm volatile("v_lshlrev_b32 %0, %1, %0" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_or, uint32_t, SEED32, asm volatile("v_or_b32 %0, %0, %1" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_or3, uint32_t, SEED32, asm volatile("v_or3_b32 %0, %0, %1, %0" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_lshladd32, uint32_t, SEED32, asm volatile("v_lshl_add_u32 %0, %0, 1, %1" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_andor, uint32_t, SEED32, asm volatile("v_and_or_b32 %0, %0, %1, %0" : "+v"(v[c]) : "v"(seed)))
+KERNEL(k_lshl64, uint64_t, (uint64_t)SEED32, asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(v[c])))
+KERNEL(k_mov64, uint64_t, (uint64_t)SEED32, asm volatile("v_mov_b64 %0, %1" : "=v"(v[c]) : "v"(v[(c + 1) % CH])))
+KERNEL(k_cmpu64, uint64_t, (uint64_t)SEED32, { uint64_t m; asm volatile("v_cmp_le_u64_e64 %0, %1, %2" : "=s"(m) : "v"(v[c]), "v"((uint64_t)seed)); })
+KERNEL(k_cmpu32, uint32_t, SEED32, { uint64_t m; asm volatile("v_cmp_ne_u32_e64 %0, %1, %2" : "=s"(m) : "v"(v[c]), "v"(seed)); })
+KERNEL(k_cndsg, uint32_t, SEED32, asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(v[c]) : "v"(seed), "s"((uint64_t)seed * 0x9E3779B97F4A7C15ull)))
+KERNEL(k_bitop3, uint32_t, SEED32, asm volatile("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96" : "+v"(v[c]) : "v"(seed)))
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ inline f2 mkf2(float a, float b) { f2 r; r.x = a; r.y = b; return r; }
 KERNEL(k_pk_fma32, f2, mkf2((float)SEED32, 1.f), asm volatile("v_pk_fma_f32 %0, %0, %1, %0" : "+v"(v[c]) : "v"(mkf2((float)seed, 2.f))))
@@ -68,6 +95,33 @@ int main() {
         {"v_min_u32", launch<uint32_t, k_min>, 1, 4},
         {"v_mad_u64_u32", launch<uint64_t, k_mad64>, 1, 8},
         {"v_lshl_add_u64", launch<uint64_t, k_lshl_add64>, 1, 8},
+        {"v_sub_u32", launch<uint32_t, k_sub>, 1, 4},
+        {"v_mov_b32", launch<uint32_t, k_mov>, 1, 4},
+        {"v_and_b32", launch<uint32_t, k_and>, 1, 4},
+        {"v_lshrrev_b32", launch<uint32_t, k_lshr>, 1, 4},
+        {"v_bfi_b32", launch<uint32_t, k_bfi>, 1, 4},
+        {"v_lshrrev_b64", launch<uint64_t, k_lshr64>, 1, 8},
+        {"v_add_co_u32", launch<uint32_t, k_addco>, 1, 4},
+        {"v_addc_co_u32", launch<uint32_t, k_addc>, 1, 4},
+        {"v_cndmask_b32", launch<uint32_t, k_cndmask>, 1, 4},
+        {"v_cmp_lt_u64+v_cndmask", launch<uint64_t, k_cmp64>, 2, 8},
+        {"v_cmp_lt_u32+v_cndmask", launch<uint32_t, k_cmp32>, 2, 4},
+        {"v_not_b32", launch<uint32_t, k_not>, 1, 4},
+        {"v_ashrrev_i32", launch<uint32_t, k_ashr>, 1, 4},
+        {"v_subrev_u32", launch<uint32_t, k_subrev>, 1, 4},
+        {"v_sub_co_u32", launch<uint32_t, k_subco>, 1, 4},
+        {"v_subb_co_u32", launch<uint32_t, k_subb>, 1, 4},
+        {"v_lshlrev_b32", launch<uint32_t, k_lshl32>, 1, 4},
+        {"v_or_b32", launch<uint32_t, k_or>, 1, 4},
+        {"v_or3_b32", launch<uint32_t, k_or3>, 1, 4},
+        {"v_lshl_add_u32", launch<uint32_t, k_lshladd32>, 1, 4},
+        {"v_and_or_b32", launch<uint32_t, k_andor>, 1, 4},
+        {"v_lshlrev_b64", launch<uint64_t, k_lshl64>, 1, 8},
+        {"v_mov_b64", launch<uint64_t, k_mov64>, 1, 8},
+        {"v_cmp_le_u64", launch<uint64_t, k_cmpu64>, 1, 8},
+        {"v_cmp_ne_u32", launch<uint32_t, k_cmpu32>, 1, 4},
+        {"v_cndmask_b32(sgpr)", launch<uint32_t, k_cndsg>, 1, 4},
+        {"v_bitop3_b32", launch<uint32_t, k_bitop3>, 1, 4},
         {"v_fma_f64", launch<double, k_fma64>, 1, 8},
         {"v_mul_f64", launch<double, k_mul64>, 1, 8},
         {"v_fma_f32", launch<float, k_fma32>, 1, 4},

@@ -108,6 +108,28 @@ def main():
                 out[c + "_frac_of_wave_cycles"] = pmc[c] / w
     if "SQ_WAVES" in pmc and "SQ_INSTS_VALU" in pmc:
         out["valu_insts_per_wave"] = pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]
+    # VALU-issue roofline inputs (tools/valu_roofline.py): the static VALU
+    # mix of this exact kernel in the library the run loaded, and the
+    # measured busy fraction where SQ_ACTIVE_INST_VALU was collected
+    if out.get("kernel_name"):
+        try:
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            import isa_mix
+
+            mix = isa_mix.valu_mix(out["kernel_name"])
+            if mix is not None:
+                out["valu_static_mix"] = dict(mix.most_common())
+        except Exception as e:  # llvm tools missing: the roofline stays null
+            out["valu_static_mix_error"] = str(e)[:200]
+    if "SQ_ACTIVE_INST_VALU" in pmc and "GRBM_GUI_ACTIVE" in pmc:
+        # SQ_ACTIVE_INST_VALU: quad-cycles (x4) in which a wave issued VALU,
+        # summed over waves; GRBM_GUI_ACTIVE: GPU-busy cycles summed over the 8
+        # XCDs (MI355X_MICROARCH.md DVFS note); 1024 SIMDs
+        cyc = pmc["GRBM_GUI_ACTIVE"] / 8
+        out["valu_busy_measured"] = 4 * pmc["SQ_ACTIVE_INST_VALU"] / (1024 * cyc)
+        kt = out.get("kernel_trace_full_batch", {}).get("avg_ns")
+        if kt:
+            out["effective_clock_ghz"] = cyc / kt
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
