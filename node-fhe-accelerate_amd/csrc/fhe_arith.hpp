@@ -87,9 +87,22 @@ __device__ __forceinline__ uint64_t umin(uint64_t a, uint64_t b) { return a < b 
 #ifndef FHE_U64_NOVCC
 #define FHE_U64_NOVCC 0
 #endif
-__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {  // (m & a) | (~m & b)
+// (m & a) | (~m & b) as gfx950's v_bitop3_b32 (LUT 0xe4 over (a, b, m)):
+// measured at full rate (111 lane-ops/CU/clk) where v_bfi_b32 issues at
+// half rate (63; tools/lab/valu_rates.hip, profiles/r6a/valu_rates_ext.txt).
+// Inline asm: written in C, LLVM turns the select of redk64 back into
+// compares and v_cndmask (more, half-rate instructions).  FHE_BFI_ASM=1:
+// the v_bfi_b32 form.
+#ifndef FHE_BFI_ASM
+#define FHE_BFI_ASM 0
+#endif
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {
     uint32_t r;
+#if FHE_BFI_ASM
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+#else
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(m));
+#endif
     return r;
 }
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));

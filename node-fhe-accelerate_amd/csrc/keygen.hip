@@ -70,7 +70,14 @@ struct Draws {
             ++blk;
             pos = 0;
         }
-        return buf[pos++];
+        // a compare chain instead of buf[pos]: a dynamically indexed local
+        // array lives in scratch (120 B per lane)
+        uint64_t r = buf[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (pos == k) r = buf[k];
+        ++pos;
+        return r;
     }
     // random_u64_range (key_manager.cpp:60-71): rejection below
     // (2^64 - max) % max, then % max

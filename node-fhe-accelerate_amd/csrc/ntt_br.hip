@@ -257,7 +257,7 @@ __device__ __forceinline__ void fwd_rest_lb(W *lds, W (&v)[LB][Geo<LOGN>::E], ui
         load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);  // in flight across the exchange
 #pragma unroll
         for (int l = 0; l < LB; ++l) lds_store<LOGN, PASS - 1>(lds + l * G::LW, v[l], tau);
-        __syncthreads();
+        xbar<lab_local<PASS - 1, PASS>()>();
 #pragma unroll
         for (int l = 0; l < LB; ++l) lds_load<LOGN, PASS>(lds + l * G::LW, v[l], tau);
         load_tw<LOGN, PASS, W, PF, 8>(tau, tw, t);

@@ -199,12 +199,29 @@ __device__ __forceinline__ void lds_load(const W *lds, W (&v)[Geo<LOGN>::E], uin
         for (int t = 0; t < (1 << R); ++t) v[t + (u << R)] = lds[base + pad_idx<LOGN>(uint32_t(t) << S)];
     }
 }
+// Lab-only timing bound (FHE_LAB_NOBAR=1, never in a shipped build: the
+// results are WRONG): the exchanges between passes >= 1 run without their
+// workgroup barriers, i.e. as if each were confined to one wave (a layout
+// whose wave bits avoid the pass digits of both passes).  Measures what
+// barrier-free exchanges could buy before any layout is redesigned.
+#ifndef FHE_LAB_NOBAR
+#define FHE_LAB_NOBAR 0
+#endif
+template <bool LOCAL>
+__device__ __forceinline__ void xbar() {
+    if constexpr (LOCAL) asm volatile("" ::: "memory");
+    else __syncthreads();
+}
+template <int PA, int PB>
+constexpr bool lab_local() { return FHE_LAB_NOBAR && PA >= 1 && PB >= 1; }
+
 // One pass exchange: registers in layout PA -> LDS -> registers in layout PB.
 // The caller's next exchange stores to the positions this one loaded from
 // (same thread, same layout), so no barrier is needed after the load.
 template <int LOGN, int PA, int PB, typename W>
 __device__ __forceinline__ void exchange(W *lds, W (&v)[Geo<LOGN>::E], uint32_t tau) {
     constexpr int E = Geo<LOGN>::E;
+    constexpr bool LOC = lab_local<PA, PB>();
     if constexpr (split_x<LOGN, W>()) {
         uint32_t *l32 = reinterpret_cast<uint32_t *>(lds);
         uint32_t h[E];
@@ -213,18 +230,18 @@ __device__ __forceinline__ void exchange(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
         lds_store<LOGN, PA>(l32, h, tau);
 #pragma unroll
         for (int e = 0; e < E; ++e) h[e] = (uint32_t)(v[e] >> 32);
-        __syncthreads();
+        xbar<LOC>();
         uint32_t lo[E];
         lds_load<LOGN, PB>(l32, lo, tau);
-        __syncthreads();  // every lane's low halves read before the high halves overwrite them
+        xbar<LOC>();  // every lane's low halves read before the high halves overwrite them
         lds_store<LOGN, PA>(l32, h, tau);
-        __syncthreads();
+        xbar<LOC>();
         lds_load<LOGN, PB>(l32, h, tau);
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = (W)lo[e] | ((W)h[e] << 32);
     } else {
         lds_store<LOGN, PA>(lds, v, tau);
-        __syncthreads();
+        xbar<LOC>();
         lds_load<LOGN, PB>(lds, v, tau);
     }
 }
@@ -661,7 +678,7 @@ __device__ __forceinline__ void fwd_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         if constexpr (stream_tw2<LOGN, W>()) {
             stream_begin<LOGN, PASS, false, false>(tau, tw, t);
             exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
-            __syncthreads();
+            xbar<lab_local<PASS - 1, PASS>()>();
             exchange<LOGN, PASS - 1, PASS>(lds, v2, tau);
             fwd_pass_stream<LOGN, PASS, LAZY, false, true>(tau, v, t, tw, ar, Scale<W>{}, &v2);
             fwd_rest2<LOGN, PASS + 1, LAZY, PF>(lds, v, v2, tau, tw, ar);
@@ -669,7 +686,7 @@ __device__ __forceinline__ void fwd_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         }
         load_tw<LOGN, PASS, W, 0, PF>(tau, tw, t);
         exchange<LOGN, PASS - 1, PASS>(lds, v, tau);
-        __syncthreads();
+        xbar<lab_local<PASS - 1, PASS>()>();
         exchange<LOGN, PASS - 1, PASS>(lds, v2, tau);
         fwd_stages2<LOGN, PASS, 0, PF, LAZY>(tau, v, v2, t, tw, ar);
         fwd_rest2<LOGN, PASS + 1, LAZY, PF>(lds, v, v2, tau, tw, ar);
@@ -997,7 +1014,7 @@ __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         if constexpr (stream_tw2<LOGN, W>()) {
             stream_begin<LOGN, PASS, true, FOLD && PASS == 0>(tau, tw, t);
             exchange<LOGN, PASS + 1, PASS>(lds, v, tau);
-            __syncthreads();
+            xbar<lab_local<PASS + 1, PASS>()>();
             exchange<LOGN, PASS + 1, PASS>(lds, v2, tau);
             inv_pass_stream<LOGN, PASS, FOLD, true>(tau, v, t, tw, ar, scale, &v2);
             inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);
@@ -1007,7 +1024,7 @@ __device__ __forceinline__ void inv_rest2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         constexpr int KS = R - PF < 0 ? 0 : R - PF;
         load_tw<LOGN, PASS, W, KS, 8>(tau, tw, t);
         exchange<LOGN, PASS + 1, PASS>(lds, v, tau);
-        __syncthreads();
+        xbar<lab_local<PASS + 1, PASS>()>();
         exchange<LOGN, PASS + 1, PASS>(lds, v2, tau);
         inv_stages2<LOGN, PASS, R - 1, R - KS, FOLD>(tau, v, v2, t, tw, ar, scale);
         inv_rest2<LOGN, PASS - 1, FOLD, PF>(lds, v, v2, tau, tw, ar, scale);

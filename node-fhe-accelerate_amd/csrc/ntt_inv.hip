@@ -7,6 +7,19 @@
 #ifndef FHE_SPLIT_X64
 #define FHE_SPLIT_X64 1
 #endif
+// Flag-free 64-bit arithmetic (fhe_arith.hpp FHE_U64_NOVCC; its bit selects
+// as full-rate v_bitop3_b32) with the carry-free mulhi (FHE_MULHI64=4: the
+// carry form cannot be combined with NOVCC in this unit -- an SGPR carry
+// the backend cannot place).  Static VALU issue cycles per wave (measured
+// rates, tools/valu_roofline.py): q62 polymul 36480 -> 34993, q62 inverse
+// 13946 -> 12544, N = 8192 64-bit polymul 38951 -> 35061, and the two
+// prime-specialised polymuls without their 6 spilled VGPRs (round 6).
+#ifndef FHE_U64_NOVCC
+#define FHE_U64_NOVCC 1
+#endif
+#ifndef FHE_MULHI64
+#define FHE_MULHI64 4
+#endif
 #include "fhe_internal.hpp"
 
 namespace FHE_NS {

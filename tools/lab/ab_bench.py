@@ -42,6 +42,22 @@ for q in [int(x) for x in args.qs.split(",")]:
     ek = fhe_gpu.EvaluationKey(ring, torch.randint(0, q, (7, 2, n), device="cuda", dtype=torch.int64, generator=g), 4)
     glwe = a[: B // 2].view(B // 4, 2, n)  # B/4 ciphertexts (k = 1)
     gout = out[: B // 2].view(B // 4, 2, n)
+    # br256: tfhe-256-secure blind rotation (N = 4096, n = 1024, (10, 3),
+    # Q_60_1), batch 64 -- only with --n 4096 --qs 1152921504606584833
+    br = None
+    if "br256" in args.ops and n == 4096:
+        be = fhe_gpu.BootstrapEngine(ring, 10, 3, 1)
+        bsk = be.prepare_ggsw(torch.randint(0, q, (1024, 6, 2, n), device="cuda", dtype=torch.int64, generator=g))
+        la = torch.randint(0, q, (64, 1024), device="cuda", dtype=torch.int64, generator=g)
+        lb = torch.randint(0, q, (64,), device="cuda", dtype=torch.int64, generator=g)
+        acc = torch.randint(0, q, (64, 2, n), device="cuda", dtype=torch.int64, generator=g)
+        acc0 = acc.clone()
+        br = (be, bsk, la, lb, acc, acc0)
+
+    def br_run():
+        be_, bsk_, la_, lb_, acc_, acc0_ = br
+        acc_.copy_(acc0_)
+        be_.blind_rotate(acc_, la_, lb_, bsk_)
     for op in args.ops.split(","):
         fn = {"fwd_mul": lambda: ring.forward_ntt_mul(a, b, out=out),
               "polymul": lambda: ring.multiply(a, b, out=out),
@@ -50,10 +66,11 @@ for q in [int(x) for x in args.qs.split(",")]:
               "ext1": lambda: eps[1](glwe, out=gout),
               "ext2": lambda: eps[2](glwe, out=gout),
               "ct_mul": lambda: eng.multiply(cx, cy, out=c3),
-              "relin": lambda: eng.relinearize(c3, ek, out=c2)}[op]
+              "relin": lambda: eng.relinearize(c3, ek, out=c2),
+              "br256": br_run}[op]
         fn()
         torch.cuda.synchronize()
-        res = {"ext1": gout, "ext2": gout, "relin": c2, "ct_mul": c3}.get(op, out)
+        res = {"ext1": gout, "ext2": gout, "relin": c2, "ct_mul": c3}.get(op, out) if op != "br256" else br[4]
         chk = int(res.sum().item()) ^ int(res[-1].sum().item())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
