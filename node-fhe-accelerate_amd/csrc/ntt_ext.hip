@@ -263,6 +263,146 @@ k_dmac(DmArgs D, NttArgs<W> A) {
     }
 }
 
+// Relinearisation at two workgroups per CU (lab build
+// FHE_RELIN2=1, measured SLOWER and not dispatched: per 16,384 ciphertexts
+// 9.11 ms with accumulator 1 in VGPRs (6 VGPRs spilled, FHE_RELIN2_ACC1G=0)
+// and 10.11 ms with both accumulators in the output rows (spill-free), against
+// 8.19 ms for k_dmac MODE 1; parity green, profiles/r6d).  k_dmac
+// MODE 1 keeps accumulator 0 in LDS beside the 64 KiB exchange (133 KB: one
+// 16-wave workgroup per CU).  Here one 512-thread workgroup per ciphertext
+// holds 32 coefficients per thread; accumulator 1 stays in VGPRs and
+// accumulator 0 lives in the ciphertext's own output row 0, used as [N] u32
+// scratch (read-modify-write of the thread's own positions, L2-resident, no
+// synchronisation) until that row's final stores -- so the LDS is the
+// exchange alone (64 KiB) and two workgroups share a CU.  c2 is re-read per
+// digit level (L2 / MALL) instead of held in VGPRs.  Same digit map,
+// Montgomery MAC, red2q accumulation and N^-1 inverse + c_j epilogue as
+// k_dmac MODE 1: bit-identical outputs.
+#ifndef FHE_RELIN2
+#define FHE_RELIN2 0
+#endif
+#ifndef FHE_RELIN2_MC
+#define FHE_RELIN2_MC 2
+#endif
+#ifndef FHE_RELIN2_PF
+#define FHE_RELIN2_PF 1
+#endif
+#ifndef FHE_RELIN2_ACC1G
+#define FHE_RELIN2_ACC1G 0
+#endif
+constexpr int kRelin2Key = gk(14, 5);
+__device__ __forceinline__ uint32_t bload32(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0);
+}
+__device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, uint32_t x) {
+    __builtin_amdgcn_raw_buffer_store_b32(x, r, vo, so, 0);
+}
+template <int K>
+__global__ void __launch_bounds__(Geo<K>::THREADS, Geo<K>::template occ_waves<uint32_t>())
+k_relin2(DmArgs D, NttArgs<uint32_t> A) {
+    using G = Geo<K>;
+    using W = uint32_t;
+    static_assert(G::P == 1 && G::E == 32, "one ciphertext per workgroup, 32 coefficients per thread");
+    constexpr int N = G::N, E = G::E, MC = FHE_RELIN2_MC, NC = E / MC;
+    __shared__ W lds[lds_elems<K, W>()];
+    const TidSource lane;
+    const size_t ct = blockIdx.x;
+    if (ct >= D.batch) return;  // whole workgroup
+    const uint64_t *srow = D.src + ct * 3 * N;
+    uint64_t *orow = D.out + ct * 2 * N;
+    const auto racc0 = brsrc(orow);  // accumulator 0: row 0 as u32 words at 4 gi
+    const auto racc1 = brsrc(orow + N);  // FHE_RELIN2_ACC1G: accumulator 1 likewise in row 1
+    const int level = D.level;
+    const uint64_t mask = (1ull << D.base_log) - 1;
+    const uint64_t q = A.q64, mu = A.mu64, lim = (uint64_t)A.ar.q2 * 2;
+    W racc[FHE_RELIN2_ACC1G ? 1 : E];
+    for (int l = 0; l < level; ++l) {
+        const uint32_t tr = lane();
+        const uint32_t shift = uint32_t(l) * uint32_t(D.base_log);
+        W v[E];
+        {
+            const auto rs = brsrc(srow + 2 * N);
+            // (SlowRed: the 32-bit-friendly exact reduction of out-of-range
+            // digits; mod64_slow's 64-bit Barrett step spills here)
+            load_coeffs_chunked<E, 8, 1>(v, lim, SlowRed<W>{A}, [&](int t) -> uint64_t {
+                return (bload(rs, tr * 8u, cbrv(t, G::LOGE) * G::T * 8u) >> shift) & mask;
+            });
+        }
+        if (l > 0) __syncthreads();  // the previous transform's last exchange reads precede these stores
+        {
+            Tw<W> t0[PassTw<K, 0>::COUNT];
+            load_tw<K, 0>(tr, A.twf, t0);
+            fwd_pass<K, 0, false>(v, t0, A.ar);
+        }
+        fwd_rest<K, 1, false, FHE_RELIN2_PF>(lds, v, tr, A.twf, A.ar);
+        // key low words (canonical prepared residues < q < 2^32): c0' takes
+        // b_l (row 1), c1' a_l (row 0); chunk c + 1 in flight while chunk c
+        // is consumed
+        const auto rb = brsrc(D.key + ((size_t)l * 2 + 1) * N), ra = brsrc(D.key + (size_t)l * 2 * N);
+        const uint32_t vo = LastIO<K>::vo(lane());
+        // one chunk in flight (nk*) while the previous one (ck*) is consumed
+        uint32_t nkb[MC], nka[MC], na0[MC], na1[MC];
+        auto issue = [&](int c) {
+#pragma unroll
+            for (int i = 0; i < MC; ++i) {
+                const uint32_t so = LastIO<K>::so(c * MC + i);
+                nkb[i] = bload32(rb, vo, so);
+                nka[i] = bload32(ra, vo, so);
+                if (l > 0) na0[i] = bload32(racc0, vo / 2u, so / 2u);
+                if (FHE_RELIN2_ACC1G && l > 0) na1[i] = bload32(racc1, vo / 2u, so / 2u);
+            }
+        };
+        issue(0);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            uint32_t ckb[MC], cka[MC], ca0[MC], ca1[MC];
+#pragma unroll
+            for (int i = 0; i < MC; ++i) ckb[i] = nkb[i], cka[i] = nka[i], ca0[i] = na0[i], ca1[i] = na1[i];
+            if (c + 1 < NC) issue(c + 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < MC; ++i) {
+                const int e = c * MC + i;
+                const uint32_t so = LastIO<K>::so(e);
+                // raw output (< 4q) times a canonical key: valid Montgomery pair
+                const W m0 = A.ar.mont(v[e], ckb[i]), m1 = A.ar.mont(v[e], cka[i]);
+                bstore32(racc0, vo / 2u, so / 2u, A.ar.red2q((l > 0 ? ca0[i] : W(0)) + m0));
+                if constexpr (FHE_RELIN2_ACC1G)
+                    bstore32(racc1, vo / 2u, so / 2u, A.ar.red2q((l > 0 ? ca1[i] : W(0)) + m1));
+                else
+                    racc[FHE_RELIN2_ACC1G ? 0 : e] = A.ar.red2q((l > 0 ? racc[FHE_RELIN2_ACC1G ? 0 : e] : W(0)) + m1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // c_j' = inv(acc_j) + c_j (encryption.cpp:953/958), row 0 first: its
+    // scratch words are read into registers before the inverse's first
+    // exchange barrier, its final stores come after the last one
+    auto fin = [&](int j) {
+        return [&, j](uint32_t gi, uint64_t x) -> uint64_t { return addq(x, red_q(srow[(size_t)j * N + gi], q, mu), q); };
+    };
+    __syncthreads();
+    {
+        const uint32_t ti = lane();
+        const uint32_t vo = LastIO<K>::vo(ti);
+        W v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = bload32(racc0, vo / 2u, LastIO<K>::so(e) / 2u);
+        inv_poly_from_regs<K, FHE_RELIN2_PF>(lds, v, ti, orow, true, A, A.ninv, 0, fin(0));
+    }
+    __syncthreads();
+    const uint32_t ti = lane();
+    if constexpr (FHE_RELIN2_ACC1G) {
+        const uint32_t vo = LastIO<K>::vo(ti);
+        W v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = bload32(racc1, vo / 2u, LastIO<K>::so(e) / 2u);
+        inv_poly_from_regs<K, FHE_RELIN2_PF>(lds, v, ti, orow + N, true, A, A.ninv, 0, fin(1));
+    } else {
+        inv_poly_from_regs<K, FHE_RELIN2_PF>(lds, racc, ti, orow + N, true, A, A.ninv, 0, fin(1));
+    }
+}
+
 // External product with one decomposition level (level == 1, K1 == 2) for
 // one polynomial per workgroup: the two digit polynomials are transformed in
 // lockstep (shared twiddles), the key MAC turns (X0, X1) into the two
@@ -362,6 +502,10 @@ static hipError_t dmac_one(const NttArgs<W> &A, hipStream_t s, int k1, const DmA
             hipLaunchKernelGGL((k_extprod2<LOGN, W>), dim3((unsigned)D.batch), dim3(G::THREADS), 0, s, D, A);
             return hipGetLastError();
         }
+    }
+    if constexpr (FHE_RELIN2 && MODE == 1 && LOGN == 14 && sizeof(W) == 4) {
+        hipLaunchKernelGGL((k_relin2<kRelin2Key>), dim3((unsigned)D.batch), dim3(Geo<kRelin2Key>::THREADS), 0, s, D, A);
+        return hipGetLastError();
     }
     // (unit twiddles, ntt_core.hpp gk_compat, measured 0 to +0.4 % here and in
     // the external-product kernels, round 5: not instantiated)
