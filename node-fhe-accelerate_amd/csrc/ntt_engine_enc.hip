@@ -1,5 +1,15 @@
 // ntt_engine_enc.hip -- EncryptionEngine::encrypt_internal
 // (encryption.cpp:171-205), batched: k_encrypt (engine_kernels.hpp).
+// Flag-free 64-bit arithmetic with the carry-free mulhi in this unit (as in
+// ntt_inv.hip; fhe_arith.hpp FHE_U64_NOVCC, FHE_MULHI64=4): fewer static VALU
+// issue cycles in its 64-bit kernels and fewer of them with scratch (round 6,
+// DESIGN.md section 5).
+#ifndef FHE_U64_NOVCC
+#define FHE_U64_NOVCC 1
+#endif
+#ifndef FHE_MULHI64
+#define FHE_MULHI64 4
+#endif
 #include "engine_kernels.hpp"
 
 namespace FHE_NS {

@@ -216,15 +216,23 @@ def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q,
     lwe_b = rnd(73, q, b)
     acc0 = rnd(74, q, b, k + 1, n)  # both components non-zero
     acc0[2, 0, :3] = [2**64 - 1, q, q + 1]  # raw words
-    got = {}
+    got, reps = {}, {}
     for pmax, pair in (("4096", "1"), ("4096", "0"), ("0", "1")):
         monkeypatch.setenv("FHE_BR_PERSIST_MAX", pmax)
         monkeypatch.setenv("FHE_BR_PAIR", pair)
+        before = be.repair_count() if k == 1 else 0
         acc = acc0.copy()
         be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
         got[pmax + pair] = acc
-    assert (got["40961"] == got["01"]).all()
-    assert (got["40960"] == got["01"]).all()
+        reps[pmax + pair] = (be.repair_count() if k == 1 else 0) - before
+    if mode == "compat" and not ((got["40961"] == got["01"]).all() and (got["40960"] == got["01"]).all()):
+        # name the path that disagrees with the oracle (and any repairs it took)
+        t = oracle.NTT(n, q)
+        exp = [t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i]) for i in range(b)]
+        bad = {p: [i for i in range(b) if not (v[i] == exp[i]).all()] for p, v in got.items()}
+        raise AssertionError(f"paths disagree: rows differing from the oracle per path {bad}, repairs {reps}")
+    assert (got["40961"] == got["01"]).all(), reps
+    assert (got["40960"] == got["01"]).all(), reps
     got["4096"] = got["40961"]
     if mode == "compat":
         t = oracle.NTT(n, q)
@@ -238,7 +246,8 @@ Q60 = 1152921504606584833    # Q_60_1, tfhe-256-secure
 
 
 @pytest.mark.parametrize("coop", ["1", "0"])
-@pytest.mark.parametrize("n,q,bl,lv", [(1024, P62, 23, 1), (2048, Q50, 15, 2), (4096, Q60, 10, 3)])
+@pytest.mark.parametrize("n,q,bl,lv", [(1024, P62, 23, 1), (2048, Q50, 15, 2), (4096, Q60, 10, 3),
+                                       (2048, 40961, 5, 2)])  # 32-bit words: the u32 repair kernel
 def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop):
     """k_br_pair with a zero poll budget: every workgroup that reaches a
     hand-off before its partner gives its ciphertext up (ABORT flag, fail

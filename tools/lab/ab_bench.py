@@ -54,6 +54,16 @@ for q in [int(x) for x in args.qs.split(",")]:
         acc0 = acc.clone()
         br = (be, bsk, la, lb, acc, acc0)
 
+    # br8192: N = 8192 (per-step k_dmac MODE 2 launches), q62, (23, 1), 64
+    # steps, batch 64 -- only with --n 8192
+    if "br8192" in args.ops and n == 8192:
+        be = fhe_gpu.BootstrapEngine(ring, 23, 1, 1)
+        bsk = be.prepare_ggsw(torch.randint(0, q, (64, 2, 2, n), device="cuda", dtype=torch.int64, generator=g))
+        la = torch.randint(0, q, (64, 64), device="cuda", dtype=torch.int64, generator=g)
+        lb = torch.randint(0, q, (64,), device="cuda", dtype=torch.int64, generator=g)
+        acc = torch.randint(0, q, (64, 2, n), device="cuda", dtype=torch.int64, generator=g)
+        br = (be, bsk, la, lb, acc, acc.clone())
+
     def br_run():
         be_, bsk_, la_, lb_, acc_, acc0_ = br
         acc_.copy_(acc0_)
@@ -67,10 +77,10 @@ for q in [int(x) for x in args.qs.split(",")]:
               "ext2": lambda: eps[2](glwe, out=gout),
               "ct_mul": lambda: eng.multiply(cx, cy, out=c3),
               "relin": lambda: eng.relinearize(c3, ek, out=c2),
-              "br256": br_run}[op]
+              "br256": br_run, "br8192": br_run}[op]
         fn()
         torch.cuda.synchronize()
-        res = {"ext1": gout, "ext2": gout, "relin": c2, "ct_mul": c3}.get(op, out) if op != "br256" else br[4]
+        res = {"ext1": gout, "ext2": gout, "relin": c2, "ct_mul": c3}.get(op, out) if not op.startswith("br") else br[4]
         chk = int(res.sum().item()) ^ int(res[-1].sum().item())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

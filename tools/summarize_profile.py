@@ -121,15 +121,21 @@ def main():
                 out["valu_static_mix"] = dict(mix.most_common())
         except Exception as e:  # llvm tools missing: the roofline stays null
             out["valu_static_mix_error"] = str(e)[:200]
-    if "SQ_ACTIVE_INST_VALU" in pmc and "GRBM_GUI_ACTIVE" in pmc:
-        # SQ_ACTIVE_INST_VALU: quad-cycles (x4) in which a wave issued VALU,
-        # summed over waves; GRBM_GUI_ACTIVE: GPU-busy cycles summed over the 8
-        # XCDs (MI355X_MICROARCH.md DVFS note); 1024 SIMDs
+    if "GRBM_GUI_ACTIVE" in pmc:
+        # GRBM_GUI_ACTIVE: GPU-busy cycles summed over the 8 XCDs
+        # (MI355X_MICROARCH.md DVFS note): the clock the kernel ran at, and the
+        # VALU instructions per CU per real cycle.  (SQ_ACTIVE_INST_VALU counts
+        # one per VALU instruction on gfx950 -- equal to SQ_INSTS_VALU on every
+        # microbenchmark kernel of profiles/r6b -- so it is no busy-cycle count.)
         cyc = pmc["GRBM_GUI_ACTIVE"] / 8
-        out["valu_busy_measured"] = 4 * pmc["SQ_ACTIVE_INST_VALU"] / (1024 * cyc)
         kt = out.get("kernel_trace_full_batch", {}).get("avg_ns")
         if kt:
             out["effective_clock_ghz"] = cyc / kt
+        if "SQ_INSTS_VALU" in pmc:
+            out["valu_insts_per_cu_cycle_measured"] = pmc["SQ_INSTS_VALU"] / (256 * cyc)
+        if "SQ_LDS_IDX_ACTIVE" in pmc:
+            # LDS-array busy cycles summed over the 256 CUs
+            out["lds_busy_frac"] = pmc["SQ_LDS_IDX_ACTIVE"] / (256 * cyc)
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -4,7 +4,8 @@ A kernel that does not stream at HBM speed is bound by the vector ALU's issue
 rate when its instruction stream, issued back to back, already takes as long
 as the kernel.  This module turns a profile summary (tools/summarize_profile.py:
 the dynamic SQ_INSTS_VALU per launch, the static VALU mix of the exact kernel
-from the shipped library, optionally SQ_ACTIVE_INST_VALU) and the measured
+from the shipped library, optionally GRBM_GUI_ACTIVE / SQ_LDS_IDX_ACTIVE for
+the clock held and the LDS-array busy share) and the measured
 per-instruction issue rates (tools/lab/valu_rates.hip on MI355X,
 profiles/r6_valu_rates.json) into:
 
@@ -116,9 +117,9 @@ def valu_roofline(summary, rates, kernel_ms=None, n_cu=N_CU, clock_ghz=CLOCK_GHZ
         out["kernel_ms"] = kernel_ms
         out["frac"] = floor_ms / kernel_ms
         out["achieved_inst_per_cu_cycle"] = insts / (n_cu * clock_ghz * 1e9 * kernel_ms * 1e-3)
-    busy = summary.get("valu_busy_measured")
-    if busy is not None:
-        out["busy_measured"] = busy
+    for k in ("effective_clock_ghz", "valu_insts_per_cu_cycle_measured", "lds_busy_frac"):
+        if summary.get(k) is not None:
+            out[k] = summary[k]
     return out
 
 
