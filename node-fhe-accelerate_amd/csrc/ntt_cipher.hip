@@ -30,6 +30,12 @@
 #ifndef FHE_STREAM_TW2
 #define FHE_STREAM_TW2 1
 #endif
+// Each transform of the 32-bit kernels re-loads its wave-uniform twiddles
+// (ntt_core.hpp opaque_tw): k_ct_mul2<1294, u32> 142 -> 10 spilled SGPRs,
+// 13 -> 5 spilled VGPRs (round 6).
+#ifndef FHE_OPAQUE_TW
+#define FHE_OPAQUE_TW 2
+#endif
 // Flag-free 64-bit arithmetic with the carry-free mulhi in this unit (as in
 // ntt_inv.hip; fhe_arith.hpp FHE_U64_NOVCC, FHE_MULHI64=4): fewer static VALU
 // issue cycles in its 64-bit kernels and fewer of them with scratch (round 6,
@@ -249,6 +255,9 @@ k_ct_mul(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64_
 #ifndef FHE_CTMUL_NOSTASH
 #define FHE_CTMUL_NOSTASH 0
 #endif
+#ifndef FHE_CTMUL2_PF32
+#define FHE_CTMUL2_PF32 1
+#endif
 template <int LOGN, typename W>
 constexpr bool ctmul_regstash() { return FHE_CTMUL_NOSTASH != 0 && sizeof(W) == 4; }
 template <int LOGN, typename W>
@@ -262,7 +271,7 @@ k_ct_mul2(const uint64_t *__restrict__ x, const uint64_t *__restrict__ y, uint64
     using G = Geo<LOGN>;
     constexpr bool RS = ctmul_regstash<LOGN, W>();
     static_assert(G::P == 1 && (G::LOGE == 5 || sizeof(W) == 8 || RS), "one ciphertext pair per workgroup");
-    constexpr int PF = sizeof(W) == 8 ? 0 : 1;  // u64: two 16-word spectra leave no VGPRs for lookahead
+    constexpr int PF = sizeof(W) == 8 ? 0 : FHE_CTMUL2_PF32;  // u64: two 16-word spectra leave no VGPRs for lookahead
     __shared__ W lds[G::LW];
     const uint32_t tau = threadIdx.x;
     const size_t poly = blockIdx.x;

@@ -154,6 +154,21 @@ struct TidSource {
     }
 };
 
+// A wave-uniform pointer the compiler may not relate to its other uses
+// (FHE_OPAQUE_TW): each transform then re-loads its wave-uniform (scalar)
+// twiddles through the constant cache instead of the compiler keeping one
+// transform's SGPR copies live across the next ones -- in kernels with
+// several transforms that CSE is what spilled SGPRs (k_ct_mul2: 142).
+#ifndef FHE_OPAQUE_TW
+#define FHE_OPAQUE_TW 0
+#endif
+// 1: every word size; 2: 32-bit words only (Tw<uint32_t>, 8 bytes).
+template <typename T>
+__device__ __forceinline__ const T *opaque_tw(const T *p) {
+    if constexpr (FHE_OPAQUE_TW == 1 || (FHE_OPAQUE_TW == 2 && sizeof(T) == 8)) asm volatile("" : "+s"(p));
+    return p;
+}
+
 __host__ __device__ constexpr uint32_t cbrv(uint32_t x, int bits) {
     uint32_t r = 0;
     for (int i = 0; i < bits; ++i) { r = (r << 1) | (x & 1); x >>= 1; }
@@ -890,8 +905,9 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
                                          bool valid, const NttArgs<W> &A, uint32_t sh = 0, H &&hook = NoHook{}, uint64_t (*pre)[Geo<LOGN>::E] = nullptr) {
     using G = Geo<LOGN>;
     constexpr bool ST = stream_tw<LOGN, W>();
+    const Tw<W> *const twf = opaque_tw(A.twf);
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
-    if constexpr (!ST) load_tw<LOGN, 0>(tau, A.twf, t0);
+    if constexpr (!ST) load_tw<LOGN, 0>(tau, twf, t0);
     // a Shoup-based first step (R-scaling) accepts any word
     const uint64_t lim = RS ? (uint64_t)(W)~W(0) : (uint64_t)(A.ar.q2 * 2);
     if (pre) {  // prefetched by the caller (load_raw)
@@ -908,12 +924,12 @@ __device__ __forceinline__ void fwd_poly(W *lds, W (&v)[Geo<LOGN>::E], uint32_t 
         });
     }
     if constexpr (ST) {
-        stream_begin<LOGN, 0, false, RS>(tau, A.twf, t0);
-        fwd_pass_stream<LOGN, 0, LAZY, RS>(tau, v, t0, A.twf, A.ar, A.rs);
+        stream_begin<LOGN, 0, false, RS>(tau, twf, t0);
+        fwd_pass_stream<LOGN, 0, LAZY, RS>(tau, v, t0, twf, A.ar, A.rs);
     } else {
         fwd_pass<LOGN, 0, LAZY, W, RS>(v, t0, A.ar, A.rs);
     }
-    fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, A.twf, A.ar, hook);
+    fwd_rest<LOGN, 1, LAZY, PF>(lds, v, tau, twf, A.ar, hook);
 }
 
 // fwd_poly for two polynomials at once (P == 1, no sub-transform offsets):
@@ -925,8 +941,9 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
     constexpr bool ST = stream_tw2<LOGN, W>();
+    const Tw<W> *const twf = opaque_tw(A.twf);
     Tw<W> t0[PassTw<LOGN, 0>::COUNT];
-    if constexpr (!ST) load_tw<LOGN, 0>(tau, A.twf, t0);
+    if constexpr (!ST) load_tw<LOGN, 0>(tau, twf, t0);
     const uint64_t lim = (uint64_t)(A.ar.q2 * 2);
     const uint32_t vo = tau * 8u;
     {
@@ -942,13 +959,13 @@ __device__ __forceinline__ void fwd_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
         });
     }
     if constexpr (ST) {
-        stream_begin<LOGN, 0, false, false>(tau, A.twf, t0);
-        fwd_pass_stream<LOGN, 0, LAZY, false, true>(tau, v, t0, A.twf, A.ar, Scale<W>{}, &v2);
+        stream_begin<LOGN, 0, false, false>(tau, twf, t0);
+        fwd_pass_stream<LOGN, 0, LAZY, false, true>(tau, v, t0, twf, A.ar, Scale<W>{}, &v2);
     } else {
         fwd_pass<LOGN, 0, LAZY, W>(v, t0, A.ar);
         fwd_pass<LOGN, 0, LAZY, W>(v2, t0, A.ar);
     }
-    fwd_rest2<LOGN, 1, LAZY, PF>(lds, v, v2, tau, A.twf, A.ar);
+    fwd_rest2<LOGN, 1, LAZY, PF>(lds, v, v2, tau, twf, A.ar);
 }
 
 // Inverse transform from v (last-pass layout, values in [0, 2q)) to HBM
@@ -967,17 +984,18 @@ __device__ __forceinline__ void inv_poly_from_regs(W *lds, W (&v)[Geo<LOGN>::E],
                                                    F &&fin = NoFin{}) {
     using G = Geo<LOGN>;
     constexpr int LAST = G::NP - 1;
+    const Tw<W> *const twi = opaque_tw(A.twi);
     {
         Tw<W> t[PassTw<LOGN, LAST>::COUNT];
         if constexpr (stream_tw<LOGN, W>()) {
-            stream_begin<LOGN, LAST, true, false>(tau, A.twi, t);
-            inv_pass_stream<LOGN, LAST, true>(tau, v, t, A.twi, A.ar, scale);
+            stream_begin<LOGN, LAST, true, false>(tau, twi, t);
+            inv_pass_stream<LOGN, LAST, true>(tau, v, t, twi, A.ar, scale);
         } else {
-            load_tw<LOGN, LAST>(tau, A.twi, t);
+            load_tw<LOGN, LAST>(tau, twi, t);
             inv_pass<LOGN, LAST, true>(v, t, A.ar, scale);
         }
     }
-    inv_rest<LOGN, LAST - 1, true, PF>(lds, v, tau, A.twi, A.ar, scale);
+    inv_rest<LOGN, LAST - 1, true, PF>(lds, v, tau, twi, A.ar, scale);
 #pragma unroll
     for (int t = 0; t < G::E; ++t) {
         const uint32_t gi = (tau + cbrv(t, G::LOGE) * G::T) << sh;
@@ -1037,19 +1055,20 @@ __device__ __forceinline__ void inv_poly2(W *lds, W (&v)[Geo<LOGN>::E], W (&v2)[
     using G = Geo<LOGN>;
     static_assert(G::P == 1, "dual transform: one polynomial pair per workgroup");
     constexpr int LAST = G::NP - 1;
+    const Tw<W> *const twi = opaque_tw(A.twi);
     {
         Tw<W> t[PassTw<LOGN, LAST>::COUNT];
         if constexpr (stream_tw2<LOGN, W>()) {
-            stream_begin<LOGN, LAST, true, false>(tau, A.twi, t);
-            inv_pass_stream<LOGN, LAST, true, true>(tau, v, t, A.twi, A.ar, scale, &v2);
+            stream_begin<LOGN, LAST, true, false>(tau, twi, t);
+            inv_pass_stream<LOGN, LAST, true, true>(tau, v, t, twi, A.ar, scale, &v2);
         } else {
             constexpr int R = PassTw<LOGN, LAST>::R;
             constexpr int KS = R - PF < 0 ? 0 : R - PF;
-            load_tw<LOGN, LAST, W, KS, 8>(tau, A.twi, t);
-            inv_stages2<LOGN, LAST, R - 1, R - KS, true>(tau, v, v2, t, A.twi, A.ar, scale);
+            load_tw<LOGN, LAST, W, KS, 8>(tau, twi, t);
+            inv_stages2<LOGN, LAST, R - 1, R - KS, true>(tau, v, v2, t, twi, A.ar, scale);
         }
     }
-    inv_rest2<LOGN, LAST - 1, true, PF>(lds, v, v2, tau, A.twi, A.ar, scale);
+    inv_rest2<LOGN, LAST - 1, true, PF>(lds, v, v2, tau, twi, A.ar, scale);
     const auto r1 = brsrc(dst), r2 = brsrc(dst2);
 #pragma unroll
     for (int t = 0; t < G::E; ++t) {
