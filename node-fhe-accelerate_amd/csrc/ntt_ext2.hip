@@ -48,6 +48,13 @@
 #ifndef FHE_EXTACC_HOOK
 #define FHE_EXTACC_HOOK 0
 #endif
+// lab: the 62-bit sparse prime compiled in (ntt_core.hpp gk_sparse), as in
+// k_extprod2 for (23, 1): 0.4 % fewer static issue
+// cycles, spill-free, but 13.33 vs 13.05 ms per 16,384 at (15, 2) (round 6,
+// profiles/r6h): not dispatched
+#ifndef FHE_EXTACC_SPARSE
+#define FHE_EXTACC_SPARSE 0
+#endif
 
 namespace FHE_NS {
 
@@ -168,8 +175,12 @@ hipError_t launch_extprod_acc(const Plan &p, int level, int base_log, const uint
     for (size_t b0 = 0; b0 < batch; b0 += per) {
         const size_t nb = batch - b0 < per ? batch - b0 : per;
         ExtAccArgs D{glwe + b0 * 2 * ((size_t)1 << 14), ggsw, out + b0 * 2 * ((size_t)1 << 14), level, base_log};
-        hipLaunchKernelGGL((k_extprod_acc<kExtAccKey>), dim3((unsigned)nb), dim3(Geo<kExtAccKey>::THREADS), 0,
-                           p.stream, D, p.a64);
+        if (FHE_EXTACC_SPARSE && p.a64.ar.sp == 1)
+            hipLaunchKernelGGL((k_extprod_acc<gk_sparse(kExtAccKey, 1)>), dim3((unsigned)nb),
+                               dim3(Geo<kExtAccKey>::THREADS), 0, p.stream, D, p.a64);
+        else
+            hipLaunchKernelGGL((k_extprod_acc<kExtAccKey>), dim3((unsigned)nb), dim3(Geo<kExtAccKey>::THREADS), 0,
+                               p.stream, D, p.a64);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
