@@ -383,6 +383,12 @@ def test_valu_roofline_arithmetic():
     assert 3.7 < r["issue_floor_ms"] < 3.85 and 0.6 < r["frac_profile"] < 0.63
     fp = vr.hbm_frac_profile(s, fx["algorithmic_bytes"])
     assert abs(fp - fx["algorithmic_bytes"] / (prof_ms * 1e-3) / 8e12) < 1e-12
+    # at the clock the kernel held (GRBM_GUI_ACTIVE / 8 per ms) the floor
+    # scales by 2.4 GHz / that clock
+    assert "issue_floor_ms_at_held_clock" not in r
+    r2 = vr.valu_roofline(dict(s, effective_clock_ghz=2.0), rates, kernel_ms=fx["event_kernel_ms"])
+    assert abs(r2["issue_floor_ms_at_held_clock"] - floor_ms * 1.2) < 1e-9 * floor_ms
+    assert abs(r2["frac_at_held_clock"] - floor_ms * 1.2 / fx["event_kernel_ms"]) < 1e-12
     # a summary without the counters or the mix gives no roofline
     assert vr.valu_roofline({"kernel_trace_full_batch": s["kernel_trace_full_batch"]}, rates) is None
     # the committed rate table parses and prices the multiplies at half rate

@@ -120,6 +120,17 @@ def valu_roofline(summary, rates, kernel_ms=None, n_cu=N_CU, clock_ghz=CLOCK_GHZ
     for k in ("effective_clock_ghz", "valu_insts_per_cu_cycle_measured", "lds_busy_frac"):
         if summary.get(k) is not None:
             out[k] = summary[k]
+    # The clock the kernel held (GRBM_GUI_ACTIVE / 8 over its duration) is
+    # below 2.4 GHz for the multiply-dense kernels (1.9-2.2 GHz): the same
+    # issue cycles take longer there, so the floor at the held clock is the
+    # bound the kernel can actually reach.
+    clk = summary.get("effective_clock_ghz")
+    if clk:
+        held = floor_ms * clock_ghz / clk
+        out["issue_floor_ms_at_held_clock"] = held
+        out["frac_profile_at_held_clock"] = held / prof_ms
+        if kernel_ms:
+            out["frac_at_held_clock"] = held / kernel_ms
     return out
 
 
