@@ -101,13 +101,17 @@ bool br_persist_supported(const Plan &p, int k1);
 // workgroup whose partner does not answer within timeout_ticks (100 MHz)
 // gives up on its ciphertext; the launch is followed by a repair pass
 // (k_br_persist) over the given-up ciphertexts, each counted in *repairs.
+// With multi set, levels 2 / 3 at small batches take 2 level CUs per
+// ciphertext instead (k_br_multi; br_multi_members), same protocol and repair.
 struct BrPairOpts {
     uint64_t timeout_ticks;
     bool coop;                     // hipLaunchCooperativeKernel (grid checked against occupancy)
     unsigned long long *repairs;   // device counter
+    bool multi;                    // k_br_multi where br_multi_members > 0
 };
 bool br_pair_supported(const Plan &p, int k1, size_t batch);
-size_t br_pair_scratch_bytes(const Plan &p, size_t batch);
+int br_multi_members(const Plan &p, int level, size_t batch);
+size_t br_pair_scratch_bytes(const Plan &p, size_t batch, int level, bool multi);
 hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc, const uint64_t *bsk,
                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q, size_t batch,
                           void *scratch, const BrPairOpts &o);

@@ -509,11 +509,17 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
             asm volatile("" : "+v"(tx));
             if constexpr (FHE_BR_PAIR_X16 && G::E >= 2 && G::E <= 8) {
                 // 16-byte sc1 stores, lane-contiguous pairs (the partner's lane
-                // tau reads exactly these words)
+                // tau reads exactly these words).  The s_nop 1 inside the asm:
+                // a store of more than 8 bytes reads its data VGPRs after
+                // issue, and the compiler's next VALU may already overwrite
+                // them (its hazard pass does not pad inline asm) -- without it
+                // a partner received an address word instead of a MAC term
+                // now and then (round 6: the intermittent pair-vs-step test
+                // failure at N = 2048, and every 64-bit k_br_multi result)
 #pragma unroll
                 for (int e = 0; e < G::E; e += 2) {
                     g64 *p = mybuf + par + 2 * ((e / 2) * T + tx);
-                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(pair128((uint64_t)xacc[e], (uint64_t)xacc[e + 1]))
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(pair128((uint64_t)xacc[e], (uint64_t)xacc[e + 1]))
                                  : "memory");
                 }
             } else {
@@ -606,6 +612,168 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
         for (int ph = 0; ph < kBrStampPhases; ++ph) X.stamps[(size_t)b * kBrStampPhases + ph] = st_sum[ph];
 #endif
     for (uint32_t i = tau; i < (uint32_t)N; i += T) gacc[i] = acc[i];
+}
+
+// Blind rotation on M = 2L CUs per ciphertext (k = 1, L = level = 2 or 3):
+// member m = (row, digit level) = (m / L, m % L) transforms ONE digit row per
+// step (k_br_pair transforms L of them), multiplies it by both key
+// components, and publishes both products; every member of row h then sums
+// component h over all M members and runs the inverse of component h itself
+// (the L members of a row hold the same accumulator row, so the inverse is
+// computed L times instead of handed out: one hand-off per step, as in the
+// pair).  The critical path of a step is one forward transform instead of L.
+// Same hand-off protocol as k_br_pair (write-through payload, drain, barrier,
+// relaxed epoch flag; bounded poll of the M - 1 partner flags by wave 0;
+// ABORT + fail[] + the host's repair pass when a partner does not answer).
+// The M workgroups of a ciphertext are blocks b, b + 8, ..., b + 8 (M - 1):
+// one XCD.  Payload per (ciphertext, member): [2 parities][2 components][N].
+template <int LOGN, typename W, int M>
+__global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_multi(BrArgs D, NttArgs<W> A, BrPairX X,
+                                                                         uint32_t batch) {
+    constexpr int K = br_pair_key<LOGN>();
+    using G = Geo<K>;
+    constexpr int N = G::N, T = G::T, L = M / 2;
+    static_assert(M == 4 || M == 6, "two or three digit levels");
+    static_assert(G::E >= 2 && G::E <= 8, "2, 4 or 8 words per lane");
+    __shared__ uint64_t acc[N];  // raw accumulator component h
+    __shared__ W lds[G::LW];     // NTT exchange
+    __shared__ uint32_t fail;
+    const uint32_t b = blockIdx.x, ct = (b / (8 * M)) * 8 + (b & 7), m = (b >> 3) % M;
+    if (ct >= batch) return;  // every member of ct takes the same branch
+    const uint32_t pl = m / L, lv = m % L;
+    const uint32_t tau = threadIdx.x;
+    const uint64_t q = A.q64, mu = A.mu64;
+    {
+        const uint64_t *gin = D.acc_in + ((size_t)ct * 2 + pl) * N;
+        const uint32_t r0 = rot_norm(-rot_amount(D.lwe_b[ct], N, D.lwe_q), N);
+        for (uint32_t i = tau; i < (uint32_t)N; i += T) acc[i] = rotated_at(gin, i, r0, N, q, mu);
+    }
+    if (tau == 0) fail = 0;
+    __syncthreads();
+    const uint64_t base = 1ull << D.base_log, mask = base - 1, half = base / 2;
+    const bool small_base = base <= q;
+    const uint32_t shift = uint32_t(L - 1 - lv) * uint32_t(D.base_log);
+    const size_t ggsw_words = (size_t)2 * L * 2 * N;
+    const size_t row = (size_t)pl * L + lv;
+    const uint64_t *lwe_a = D.lwe_a + (size_t)ct * D.lwe_dim;
+    g32 *const flags = (g32 *)(X.flag + (size_t)ct * M);
+    g64 *const mybuf = (g64 *)(X.buf + ((size_t)ct * M + m) * 4 * N);
+    bool canon = false;
+    uint32_t epoch = 0;
+    for (uint32_t step = 0; step < D.lwe_dim; ++step) {
+        const int32_t r = rot_amount(lwe_a[step], N, D.lwe_q);  // uniform, and equal in every member
+        if (r == 0) continue;
+        const uint32_t rot = rot_norm(r, N);
+        const uint64_t *key = D.bsk + ggsw_words * step;
+        W oacc[G::E], xacc[G::E];
+        {
+            uint64_t kv[2][G::E];
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const uint32_t gi = gidx<K, G::NP - 1>(tau, e);
+                kv[0][e] = key[(row * 2 + pl) * N + gi];
+                kv[1][e] = key[(row * 2 + (1 - pl)) * N + gi];
+            }
+            uint32_t tr = tau;
+            asm volatile("" : "+v"(tr));
+            W v[1][G::E];
+            Tw<W> t0[PassTw<K, 0>::COUNT];
+            load_tw<K, 0>(tr, A.twf, t0);
+            load_coeffs<G::E>(v[0], (uint64_t)A.ar.q2 * 2, q, mu, [&](int t) -> uint64_t {
+                const uint32_t p = tr + cbrv(t, G::LOGE) * T;
+                const uint32_t j = (p + 2 * N - rot) & (2 * N - 1);
+                uint64_t df;
+                if (canon) {
+                    const uint64_t a = acc[j < (uint32_t)N ? j : j - N];
+                    const uint64_t xr = j < (uint32_t)N || a == 0 ? a : q - a;
+                    df = subq(xr, acc[p], q);
+                } else {
+                    const uint64_t xr = j < (uint32_t)N ? acc[j] : red_q(q - acc[j - N], q, mu);
+                    df = subq(red_q(xr, q, mu), red_q(acc[p], q, mu), q);
+                }
+                uint64_t d = (df >> shift) & mask;
+                if (d > half) d = small_base ? q - (base - d) : red_q(q - (base - d), q, mu);
+                return d;
+            });
+            fwd_pass<K, 0, false>(v[0], t0, A.ar);
+            fwd_rest_lb<K, 1, 1, kPfSingle>(lds, v, tr, A.twf, A.ar);
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                oacc[e] = A.ar.mont(v[0][e], (W)kv[0][e]);
+                xacc[e] = A.ar.mont(v[0][e], (W)kv[1][e]);
+            }
+        }
+        ++epoch;
+        const uint32_t par = (epoch & 1) * 2 * N;
+        {
+            // slot c of this member = its product for output component c
+            uint32_t tx = tau;
+            asm volatile("" : "+v"(tx));
+#pragma unroll
+            for (int e = 0; e < G::E; e += 2) {
+                g64 *p0 = mybuf + par + pl * N + 2 * ((e / 2) * T + tx);
+                g64 *p1 = mybuf + par + (1 - pl) * N + 2 * ((e / 2) * T + tx);
+                asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p0), "v"(pair128((uint64_t)oacc[e], (uint64_t)oacc[e + 1]))
+                             : "memory");
+                asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p1), "v"(pair128((uint64_t)xacc[e], (uint64_t)xacc[e + 1]))
+                             : "memory");
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        if (tau == 0) __hip_atomic_store(flags + m, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tau < 64) {  // wave 0: lane i polls member i, for at most X.timeout
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            bool ok = false;
+            for (;;) {
+                uint32_t f = epoch;
+                if (tau < (uint32_t)M && tau != m)
+                    f = __hip_atomic_load(flags + tau, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool ab = (f & kBrAbort) != 0;
+                if (__ballot(ab)) break;  // a member gave up
+                if (__ballot(f < epoch) == 0 && X.timeout != 0) {  // zero budget: the tests' never-answering partner
+                    ok = true;
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 >= X.timeout) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!ok && tau == 0) {
+                fail = 1;
+                __hip_atomic_store(flags + m, kBrAbort | epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((g32 *)(X.fail + ct), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (fail) return;  // workgroup-uniform: nothing stored, the repair pass recomputes ct
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+        uint32_t ti = tau;
+        asm volatile("" : "+v"(ti));
+#pragma unroll
+        for (int o = 1; o < M; ++o) {
+            const uint32_t pm = (m + o) % M;
+            const g64 *src = (const g64 *)(X.buf + ((size_t)ct * M + pm) * 4 * N) + par + pl * N;
+#pragma unroll
+            for (int e = 0; e < G::E; ++e) {
+                const W x = (W)__hip_atomic_load(src + 2 * ((e / 2) * T + ti) + (e & 1), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                oacc[e] = A.ar.red2q(oacc[e] + x);
+            }
+        }
+        // component h: inverse, then acc_h = mod_add(inv, red_q(acc_h))
+        inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
+                                                [&](uint32_t gi, uint64_t x) -> uint64_t {
+                                                    const uint64_t a = acc[gi];
+                                                    acc[gi] = addq(x, canon ? a : red_q(a, q, mu), q);
+                                                    return 0;
+                                                });
+        __syncthreads();
+        canon = true;
+    }
+    if (lv == 0) {
+        uint64_t *gacc = D.acc + ((size_t)ct * 2 + pl) * N;
+        for (uint32_t i = tau; i < (uint32_t)N; i += T) gacc[i] = acc[i];
+    }
 }
 
 // GLWE dimension k >= 2 (K1 = k + 1 >= 3 accumulators): the same one-launch
@@ -837,12 +1005,25 @@ bool br_pair_supported(const Plan &p, int k1, size_t batch) {
     if (p.wide || k1 != 2 || p.logn < 10 || p.logn > 12 || batch == 0) return false;
     return 16 * ((batch + 7) / 8) <= (size_t)p.cus;
 }
-// scratch: flags [batch][2] u32 + fail [batch] u32 (16-byte aligned), the
-// saved input accumulators [batch][2][N], the hand-off buffers [batch][2][2][N]
-static size_t br_pair_flag_bytes(size_t batch) { return ((batch * 3 * 4 + 15) / 16) * 16; }
-size_t br_pair_scratch_bytes(const Plan &p, size_t batch) {
+// M = 2 level CUs per ciphertext (k_br_multi) when every ciphertext's M
+// workgroups fit one XCD beside the others dealt to it: 8 ceil(batch / 8)
+// ciphertexts' worth of blocks, M ceil(batch / 8) per XCD; 0 = the pair.
+int br_multi_members(const Plan &p, int level, size_t batch) {
+    if (p.wide || level < 2 || level > 3 || p.logn < 10 || p.logn > 12 || batch == 0) return 0;
+    const int M = 2 * level;
+    return (size_t)M * ((batch + 7) / 8) <= (size_t)p.cus / 8 ? M : 0;
+}
+// scratch: flags [batch][M] u32 + fail [batch] u32 (16-byte aligned), the
+// saved input accumulators [batch][2][N], the hand-off buffers
+// [batch][M][2 parities][2 components][N] (pair: [batch][2][2][N])
+static size_t br_pair_flag_bytes(size_t batch, int members) {
+    return ((batch * (members + 1) * 4 + 15) / 16) * 16;
+}
+size_t br_pair_scratch_bytes(const Plan &p, size_t batch, int level, bool multi) {
     const size_t n = (size_t)1 << p.logn;
-    return br_pair_flag_bytes(batch) + batch * 2 * n * 8 + batch * 2 * 2 * n * 8;
+    const int M = multi ? br_multi_members(p, level, batch) : 0;
+    const size_t xbuf = M ? batch * M * 4 * n * 8 : batch * 2 * 2 * n * 8;
+    return br_pair_flag_bytes(batch, M ? M : 2) + batch * 2 * n * 8 + xbuf;
 }
 template <int LOGN, typename W, int LB>
 static hipError_t br_pair_lb_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
@@ -865,11 +1046,21 @@ static hipError_t br_pair_lb_one(const Plan &p, const BrArgs &D, const BrPairX &
     return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W, LB>, dim3(grid), block, args, PAD,
                                       p.stream);
 }
+template <int LOGN, typename W, int M>
+static hipError_t br_multi_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A) {
+    constexpr int PAD = br_pair_pad_lds<LOGN, W, 1>();
+    const unsigned grid = (unsigned)(8 * M * ((batch + 7) / 8));
+    hipLaunchKernelGGL((k_br_multi<LOGN, W, M>), dim3(grid), dim3(Geo<br_pair_key<LOGN>()>::T), PAD, p.stream, D, A,
+                       X, (uint32_t)batch);
+    return hipGetLastError();
+}
 // Lockstep width for `level` levels: the LB <= br_pair_lb() with the fewest
 // idle (zero) transforms, the widest among equals.
 template <int LOGN, typename W>
 static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
-                              bool coop) {
+                              bool coop, int members) {
+    if (members == 4) return br_multi_one<LOGN, W, 4>(p, D, X, batch, A);
+    if (members == 6) return br_multi_one<LOGN, W, 6>(p, D, X, batch, A);
     constexpr int LM = br_pair_lb<LOGN, W>();
     int lb = 1, best = 1 << 30;
     for (int c = 1; c <= LM; ++c) {
@@ -886,23 +1077,23 @@ static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, 
 }
 template <typename W>
 static hipError_t br_pair_dispatch(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch,
-                                   const NttArgs<W> &A, bool coop) {
+                                   const NttArgs<W> &A, bool coop, int members) {
     // 64-bit words in compat mode (the TFHE presets' moduli): unit twiddles
     // in pass 0 (ntt_core.hpp gk_compat)
     if constexpr (sizeof(W) == 8) {
         if (p.compat) {
             switch (p.logn) {
-            case 10: return br_pair_one<gk_compat(10), W>(p, D, X, batch, A, coop);
-            case 11: return br_pair_one<gk_compat(11), W>(p, D, X, batch, A, coop);
-            case 12: return br_pair_one<gk_compat(12), W>(p, D, X, batch, A, coop);
+            case 10: return br_pair_one<gk_compat(10), W>(p, D, X, batch, A, coop, members);
+            case 11: return br_pair_one<gk_compat(11), W>(p, D, X, batch, A, coop, members);
+            case 12: return br_pair_one<gk_compat(12), W>(p, D, X, batch, A, coop, members);
             default: return hipErrorInvalidValue;
             }
         }
     }
     switch (p.logn) {
-    case 10: return br_pair_one<10, W>(p, D, X, batch, A, coop);
-    case 11: return br_pair_one<11, W>(p, D, X, batch, A, coop);
-    case 12: return br_pair_one<12, W>(p, D, X, batch, A, coop);
+    case 10: return br_pair_one<10, W>(p, D, X, batch, A, coop, members);
+    case 11: return br_pair_one<11, W>(p, D, X, batch, A, coop, members);
+    case 12: return br_pair_one<12, W>(p, D, X, batch, A, coop, members);
     default: return hipErrorInvalidValue;
     }
 }
@@ -910,8 +1101,10 @@ hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc,
                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q, size_t batch,
                           void *scratch, const BrPairOpts &o) {
     if (!br_pair_supported(p, 2, batch)) return hipErrorInvalidValue;
-    const size_t n = (size_t)1 << p.logn, fbytes = br_pair_flag_bytes(batch), abytes = batch * 2 * n * 8;
-    uint32_t *flag = (uint32_t *)scratch, *failw = flag + batch * 2;
+    const int members = o.multi ? br_multi_members(p, level, batch) : 0;
+    const size_t n = (size_t)1 << p.logn, fbytes = br_pair_flag_bytes(batch, members ? members : 2),
+                 abytes = batch * 2 * n * 8;
+    uint32_t *flag = (uint32_t *)scratch, *failw = flag + batch * (members ? members : 2);
     uint64_t *acc_in = (uint64_t *)((char *)scratch + fbytes);
     uint64_t *buf = acc_in + batch * 2 * n;
     hipError_t e = hipMemsetAsync(scratch, 0, fbytes, p.stream);  // flags and fail words, every launch
@@ -926,8 +1119,8 @@ hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc,
     if (sv && sv[0] == '1' && hipMalloc(&X.stamps, grid * kBrStampPhases * 8) == hipSuccess)
         (void)hipMemsetAsync(X.stamps, 0, grid * kBrStampPhases * 8, p.stream);
 #endif
-    e = p.word == 32 ? br_pair_dispatch<uint32_t>(p, D, X, batch, p.a32, o.coop)
-                     : br_pair_dispatch<uint64_t>(p, D, X, batch, p.a64, o.coop);
+    e = p.word == 32 ? br_pair_dispatch<uint32_t>(p, D, X, batch, p.a32, o.coop, members)
+                     : br_pair_dispatch<uint64_t>(p, D, X, batch, p.a64, o.coop, members);
 #if FHE_BR_STAMPS
     if (X.stamps) {
         std::vector<uint64_t> h(grid * kBrStampPhases);

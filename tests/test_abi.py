@@ -171,7 +171,7 @@ SCRATCH_FREE = [
     "k_ntt_inv<14, unsigned int>", "k_ntt_inv<14, unsigned long>",
     "k_extprod_acc<", "k_extprod2<14, unsigned long>", "k_br_persist<", "k_decrypt<",
     # round 4: the two-CU blind rotation, k = 2..4 single launch, the RNS limb kernels
-    "k_br_pair<", "k_br_persist_k<", "k_ntt_fwd_limbs<", "k_ntt_inv_limbs<", "k_polymul_limbs<",
+    "k_br_pair<", "k_br_multi<", "k_br_persist_k<", "k_ntt_fwd_limbs<", "k_ntt_inv_limbs<", "k_polymul_limbs<",
     "k_polymul2_limbs<",
 ]
 # Measured exceptions inside SCRATCH_FREE's patterns, each pinned to its

@@ -217,21 +217,27 @@ def test_blind_rotate_single_launch_matches_step_launches(fg, monkeypatch, n, q,
     acc0 = rnd(74, q, b, k + 1, n)  # both components non-zero
     acc0[2, 0, :3] = [2**64 - 1, q, q + 1]  # raw words
     got, reps = {}, {}
-    for pmax, pair in (("4096", "1"), ("4096", "0"), ("0", "1")):
+    # "40961": 2 lv CUs per ciphertext (k_br_multi) at lv = 2 / 3, the pair
+    # at lv = 1; "40961p": the pair (FHE_BR_MULTI=0)
+    for pmax, pair, multi in (("4096", "1", "1"), ("4096", "1", "0"), ("4096", "0", "1"), ("0", "1", "1")):
         monkeypatch.setenv("FHE_BR_PERSIST_MAX", pmax)
         monkeypatch.setenv("FHE_BR_PAIR", pair)
+        monkeypatch.setenv("FHE_BR_MULTI", multi)
+        key = pmax + pair + ("" if multi == "1" else "p")
         before = be.repair_count() if k == 1 else 0
         acc = acc0.copy()
         be.blind_rotate(acc, lwe_a, lwe_b, bsk_ntt)
-        got[pmax + pair] = acc
-        reps[pmax + pair] = (be.repair_count() if k == 1 else 0) - before
-    if mode == "compat" and not ((got["40961"] == got["01"]).all() and (got["40960"] == got["01"]).all()):
+        got[key] = acc
+        reps[key] = (be.repair_count() if k == 1 else 0) - before
+    monkeypatch.delenv("FHE_BR_MULTI")
+    if mode == "compat" and not all((got[x] == got["01"]).all() for x in ("40961", "40961p", "40960")):
         # name the path that disagrees with the oracle (and any repairs it took)
         t = oracle.NTT(n, q)
         exp = [t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i]) for i in range(b)]
         bad = {p: [i for i in range(b) if not (v[i] == exp[i]).all()] for p, v in got.items()}
         raise AssertionError(f"paths disagree: rows differing from the oracle per path {bad}, repairs {reps}")
     assert (got["40961"] == got["01"]).all(), reps
+    assert (got["40961p"] == got["01"]).all(), reps
     assert (got["40960"] == got["01"]).all(), reps
     got["4096"] = got["40961"]
     if mode == "compat":
@@ -245,15 +251,15 @@ Q50 = 1125899906826241      # Q_50_1 (parameter_set.cpp), tfhe-128-balanced
 Q60 = 1152921504606584833    # Q_60_1, tfhe-256-secure
 
 
-@pytest.mark.parametrize("coop", ["1", "0"])
+@pytest.mark.parametrize("coop,multi", [("1", "0"), ("0", "0"), ("0", "1")])
 @pytest.mark.parametrize("n,q,bl,lv", [(1024, P62, 23, 1), (2048, Q50, 15, 2), (4096, Q60, 10, 3),
                                        (2048, 40961, 5, 2)])  # 32-bit words: the u32 repair kernel
-def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop):
-    """k_br_pair with a zero poll budget: every workgroup that reaches a
-    hand-off before its partner gives its ciphertext up (ABORT flag, fail
-    word, nothing stored), and the repair pass recomputes those from the
-    saved input -- the result still equals the one-CU kernel and the oracle,
-    and the repairs are counted."""
+def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop, multi):
+    """k_br_pair (and, with multi at lv = 2 / 3, k_br_multi) with a zero poll
+    budget: every workgroup that reaches a hand-off before its partners gives
+    its ciphertext up (ABORT flag, fail word, nothing stored), and the repair
+    pass recomputes those from the saved input -- the result still equals the
+    one-CU kernel and the oracle, and the repairs are counted."""
     k, b, dim = 1, 6, 20
     r = fg.PolynomialRing(n, q)
     be = fg.BootstrapEngine(r, bl, lv, k)
@@ -268,6 +274,7 @@ def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop):
     be.blind_rotate(ref, lwe_a, lwe_b, bsk_ntt)
     monkeypatch.setenv("FHE_BR_PAIR", "1")
     monkeypatch.setenv("FHE_BR_PAIR_COOP", coop)
+    monkeypatch.setenv("FHE_BR_MULTI", multi)
     monkeypatch.setenv("FHE_BR_PAIR_TIMEOUT_US", "0")
     before = be.repair_count()
     acc = acc0.copy()
@@ -287,13 +294,14 @@ def test_br_pair_timeout_takes_repair_pass(fg, monkeypatch, n, q, bl, lv, coop):
     assert (acc == ref).all() and be.repair_count() == before
 
 
-@pytest.mark.parametrize("b", [37, 100])
+@pytest.mark.parametrize("b", [37, 64, 65, 100])
 def test_br_pair_ragged_batches(fg, monkeypatch, b):
-    """Batches that fill the two-CU grid (16 workgroups per 8 ciphertexts,
-    ct = (block >> 4) * 8 + (block & 7)) only partly: the workgroups past the
-    batch leave at once and every ciphertext equals the one-CU kernel's, rows
-    0 and b - 1 the oracle's (tfhe-128-balanced shape, compat mode: the
-    unit-twiddle kernels)."""
+    """Batches that fill the multi-CU grid (b <= 64 at lv = 2: 32 workgroups
+    per 8 ciphertexts, ct = (block / 32) * 8 + (block & 7)) or the two-CU grid
+    (16 per 8, b > 64) only partly: the workgroups past the batch leave at
+    once and every ciphertext equals the one-CU kernel's, rows 0 and b - 1 the
+    oracle's (tfhe-128-balanced shape, compat mode: the unit-twiddle
+    kernels)."""
     n, q, bl, lv, k, dim = 2048, Q50, 15, 2, 1, 6
     r = fg.PolynomialRing(n, q)
     be = fg.BootstrapEngine(r, bl, lv, k)
@@ -313,17 +321,18 @@ def test_br_pair_ragged_batches(fg, monkeypatch, b):
         assert (got["1"][i] == t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])).all(), i
 
 
-@pytest.mark.parametrize("serial", ["1", "0"])
-def test_br_pair_concurrent_contexts(fg, monkeypatch, serial):
+@pytest.mark.parametrize("serial,b", [("1", 128), ("0", 128), ("1", 40), ("0", 40)])
+def test_br_pair_concurrent_contexts(fg, monkeypatch, serial, b):
     """Two contexts run two-CU blind rotations on two streams at once, with
     grids that together need twice the CUs (2 x 256 workgroups at batch
     128).  Serialised (the default) the launches queue behind each other;
     with FHE_BR_PAIR_SERIAL=0 they may interleave, and a pair that is not
     co-resident in time goes to the repair pass.  Either way both results
-    are exact (vs the one-CU kernel, and rows vs the oracle)."""
+    are exact (vs the one-CU kernel, and rows vs the oracle).  At batch 40
+    the same on six CUs per ciphertext (k_br_multi: 2 x 240 workgroups)."""
     import torch
 
-    n, q, bl, lv, dim, k, b = 4096, Q60, 10, 3, 12, 1, 128
+    n, q, bl, lv, dim, k = 4096, Q60, 10, 3, 12, 1
     monkeypatch.setenv("FHE_BR_PAIR_SERIAL", serial)
     monkeypatch.setenv("FHE_BR_PAIR_TIMEOUT_US", "3000")
     rings = [fg.PolynomialRing(n, q) for _ in range(2)]
