@@ -627,10 +627,18 @@ __global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_pair(BrArgs 
 // ABORT + fail[] + the host's repair pass when a partner does not answer).
 // The M workgroups of a ciphertext are blocks b, b + 8, ..., b + 8 (M - 1):
 // one XCD.  Payload per (ciphertext, member): [2 parities][2 components][N].
-template <int LOGN, typename W, int M>
-__global__ void __launch_bounds__(Geo<br_pair_key<LOGN>()>::T) k_br_multi(BrArgs D, NttArgs<W> A, BrPairX X,
-                                                                         uint32_t batch) {
-    constexpr int K = br_pair_key<LOGN>();
+// Dense form (DN): two workgroups per CU (8 coefficients per thread, no LDS
+// pad), for batches whose M workgroups per ciphertext exceed one per CU.
+template <int LOGN, bool DN>
+constexpr int br_multi_key() { return DN ? gk(LOGN, 3) : br_pair_key<LOGN>(); }
+template <int LOGN, bool DN>
+constexpr int br_multi_threads() { return Geo<br_multi_key<LOGN, DN>()>::T; }
+template <int LOGN, bool DN>
+constexpr int br_multi_waves() { return DN ? 2 * br_multi_threads<LOGN, DN>() / 256 : 1; }
+template <int LOGN, typename W, int M, bool DN>
+__global__ void __launch_bounds__((br_multi_threads<LOGN, DN>()), (br_multi_waves<LOGN, DN>()))
+    k_br_multi(BrArgs D, NttArgs<W> A, BrPairX X, uint32_t batch) {
+    constexpr int K = br_multi_key<LOGN, DN>();
     using G = Geo<K>;
     constexpr int N = G::N, T = G::T, L = M / 2;
     static_assert(M == 4 || M == 6, "two or three digit levels");
@@ -1007,11 +1015,21 @@ bool br_pair_supported(const Plan &p, int k1, size_t batch) {
 }
 // M = 2 level CUs per ciphertext (k_br_multi) when every ciphertext's M
 // workgroups fit one XCD beside the others dealt to it: 8 ceil(batch / 8)
-// ciphertexts' worth of blocks, M ceil(batch / 8) per XCD; 0 = the pair.
+// ciphertexts' worth of blocks, M ceil(batch / 8) per XCD, one per CU; up to
+// twice that in the dense form (two per CU, kBrMultiDense bit); 0 = the pair.
+// (The dense form measured slower than the pair: tfhe-256-secure at batch 64
+// 32.6 vs 28.2 ms, round 6, profiles/r6r; lab FHE_BR_MULTI_DENSE=1, parity
+// green in the blind-rotation suite.)
+#ifndef FHE_BR_MULTI_DENSE
+#define FHE_BR_MULTI_DENSE 0
+#endif
+constexpr int kBrMultiDense = 0x100;
 int br_multi_members(const Plan &p, int level, size_t batch) {
     if (p.wide || level < 2 || level > 3 || p.logn < 10 || p.logn > 12 || batch == 0) return 0;
     const int M = 2 * level;
-    return (size_t)M * ((batch + 7) / 8) <= (size_t)p.cus / 8 ? M : 0;
+    const size_t per_xcd = (size_t)M * ((batch + 7) / 8), cus = (size_t)p.cus / 8;
+    if (per_xcd <= cus) return M;
+    return FHE_BR_MULTI_DENSE && per_xcd <= 2 * cus ? (M | kBrMultiDense) : 0;
 }
 // scratch: flags [batch][M] u32 + fail [batch] u32 (16-byte aligned), the
 // saved input accumulators [batch][2][N], the hand-off buffers
@@ -1021,7 +1039,7 @@ static size_t br_pair_flag_bytes(size_t batch, int members) {
 }
 size_t br_pair_scratch_bytes(const Plan &p, size_t batch, int level, bool multi) {
     const size_t n = (size_t)1 << p.logn;
-    const int M = multi ? br_multi_members(p, level, batch) : 0;
+    const int M = multi ? br_multi_members(p, level, batch) & 0xff : 0;
     const size_t xbuf = M ? batch * M * 4 * n * 8 : batch * 2 * 2 * n * 8;
     return br_pair_flag_bytes(batch, M ? M : 2) + batch * 2 * n * 8 + xbuf;
 }
@@ -1046,12 +1064,12 @@ static hipError_t br_pair_lb_one(const Plan &p, const BrArgs &D, const BrPairX &
     return hipLaunchCooperativeKernel((const void *)k_br_pair<LOGN, W, LB>, dim3(grid), block, args, PAD,
                                       p.stream);
 }
-template <int LOGN, typename W, int M>
+template <int LOGN, typename W, int M, bool DN>
 static hipError_t br_multi_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A) {
-    constexpr int PAD = br_pair_pad_lds<LOGN, W, 1>();
+    constexpr int PAD = DN ? 0 : br_pair_pad_lds<LOGN, W, 1>();
     const unsigned grid = (unsigned)(8 * M * ((batch + 7) / 8));
-    hipLaunchKernelGGL((k_br_multi<LOGN, W, M>), dim3(grid), dim3(Geo<br_pair_key<LOGN>()>::T), PAD, p.stream, D, A,
-                       X, (uint32_t)batch);
+    hipLaunchKernelGGL((k_br_multi<LOGN, W, M, DN>), dim3(grid), dim3(br_multi_threads<LOGN, DN>()), PAD,
+                       p.stream, D, A, X, (uint32_t)batch);
     return hipGetLastError();
 }
 // Lockstep width for `level` levels: the LB <= br_pair_lb() with the fewest
@@ -1059,8 +1077,13 @@ static hipError_t br_multi_one(const Plan &p, const BrArgs &D, const BrPairX &X,
 template <int LOGN, typename W>
 static hipError_t br_pair_one(const Plan &p, const BrArgs &D, const BrPairX &X, size_t batch, const NttArgs<W> &A,
                               bool coop, int members) {
-    if (members == 4) return br_multi_one<LOGN, W, 4>(p, D, X, batch, A);
-    if (members == 6) return br_multi_one<LOGN, W, 6>(p, D, X, batch, A);
+    switch (members) {
+    case 4: return br_multi_one<LOGN, W, 4, false>(p, D, X, batch, A);
+    case 6: return br_multi_one<LOGN, W, 6, false>(p, D, X, batch, A);
+    case 4 | kBrMultiDense: return br_multi_one<LOGN, W, 4, true>(p, D, X, batch, A);
+    case 6 | kBrMultiDense: return br_multi_one<LOGN, W, 6, true>(p, D, X, batch, A);
+    default: break;
+    }
     constexpr int LM = br_pair_lb<LOGN, W>();
     int lb = 1, best = 1 << 30;
     for (int c = 1; c <= LM; ++c) {
@@ -1101,10 +1124,9 @@ hipError_t launch_br_pair(const Plan &p, int level, int base_log, uint64_t *acc,
                           const uint64_t *lwe_a, const uint64_t *lwe_b, uint32_t lwe_dim, uint64_t lwe_q, size_t batch,
                           void *scratch, const BrPairOpts &o) {
     if (!br_pair_supported(p, 2, batch)) return hipErrorInvalidValue;
-    const int members = o.multi ? br_multi_members(p, level, batch) : 0;
-    const size_t n = (size_t)1 << p.logn, fbytes = br_pair_flag_bytes(batch, members ? members : 2),
-                 abytes = batch * 2 * n * 8;
-    uint32_t *flag = (uint32_t *)scratch, *failw = flag + batch * (members ? members : 2);
+    const int members = o.multi ? br_multi_members(p, level, batch) : 0, nm = members ? members & 0xff : 2;
+    const size_t n = (size_t)1 << p.logn, fbytes = br_pair_flag_bytes(batch, nm), abytes = batch * 2 * n * 8;
+    uint32_t *flag = (uint32_t *)scratch, *failw = flag + batch * nm;
     uint64_t *acc_in = (uint64_t *)((char *)scratch + fbytes);
     uint64_t *buf = acc_in + batch * 2 * n;
     hipError_t e = hipMemsetAsync(scratch, 0, fbytes, p.stream);  // flags and fail words, every launch

@@ -321,7 +321,7 @@ def test_br_pair_ragged_batches(fg, monkeypatch, b):
         assert (got["1"][i] == t.blind_rotate(k, bl, lv, lwe_a[i], int(lwe_b[i]), q, bsk, acc0[i])).all(), i
 
 
-@pytest.mark.parametrize("serial,b", [("1", 128), ("0", 128), ("1", 40), ("0", 40)])
+@pytest.mark.parametrize("serial,b", [("1", 128), ("0", 128), ("1", 40), ("0", 40), ("1", 64), ("0", 64)])
 def test_br_pair_concurrent_contexts(fg, monkeypatch, serial, b):
     """Two contexts run two-CU blind rotations on two streams at once, with
     grids that together need twice the CUs (2 x 256 workgroups at batch
@@ -329,7 +329,8 @@ def test_br_pair_concurrent_contexts(fg, monkeypatch, serial, b):
     with FHE_BR_PAIR_SERIAL=0 they may interleave, and a pair that is not
     co-resident in time goes to the repair pass.  Either way both results
     are exact (vs the one-CU kernel, and rows vs the oracle).  At batch 40
-    the same on six CUs per ciphertext (k_br_multi: 2 x 240 workgroups)."""
+    the same on six CUs per ciphertext (k_br_multi: 2 x 240 workgroups), at
+    batch 64 in its dense form (two workgroups per CU: 2 x 384)."""
     import torch
 
     n, q, bl, lv, dim, k = 4096, Q60, 10, 3, 12, 1
@@ -502,7 +503,7 @@ def test_key_switch_split_vs_oracle(fg, q, bl, lv, in_dim, out_dim, b):
 
 @pytest.mark.parametrize("name,n,q,bl,lv", [("tfhe-128-balanced", 2048, Q50, 15, 2),
                                              ("tfhe-256-secure", 4096, Q60, 10, 3)])
-@pytest.mark.parametrize("b", [1, 5])
+@pytest.mark.parametrize("b", [1, 5, 64])  # 64: tfhe-256 on the dense multi-CU form
 def test_bootstrap_presets_vs_oracle(fg, name, n, q, bl, lv, b):
     """fhe_bootstrap_batch (bootstrap_with_test_poly, bootstrap_engine.cpp:
     684-711: blind rotation on two CUs per ciphertext, sample extract, key
