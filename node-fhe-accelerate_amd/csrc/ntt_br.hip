@@ -711,6 +711,14 @@ __global__ void __launch_bounds__((br_multi_threads<LOGN, DN>()), (br_multi_wave
                 xacc[e] = A.ar.mont(v[0][e], (W)kv[1][e]);
             }
         }
+#ifndef FHE_BR_MULTI_INVPF
+#define FHE_BR_MULTI_INVPF 1
+#endif
+        // the inverse's first-pass twiddles, in flight across the hand-off
+        // (inv_poly_from_regs would load them after it)
+        constexpr int LAST = G::NP - 1;
+        Tw<W> tl[PassTw<K, LAST>::COUNT];
+        if constexpr (FHE_BR_MULTI_INVPF) load_tw<K, LAST>(tau, A.twi, tl);
         ++epoch;
         const uint32_t par = (epoch & 1) * 2 * N;
         {
@@ -769,12 +777,23 @@ __global__ void __launch_bounds__((br_multi_threads<LOGN, DN>()), (br_multi_wave
             }
         }
         // component h: inverse, then acc_h = mod_add(inv, red_q(acc_h))
-        inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
-                                                [&](uint32_t gi, uint64_t x) -> uint64_t {
-                                                    const uint64_t a = acc[gi];
-                                                    acc[gi] = addq(x, canon ? a : red_q(a, q, mu), q);
-                                                    return 0;
-                                                });
+        if constexpr (FHE_BR_MULTI_INVPF && !stream_tw<K, W>()) {
+            inv_pass<K, LAST, true>(oacc, tl, A.ar, A.ninv);
+            inv_rest<K, LAST - 1, true, kPfSingle>(lds, oacc, ti, A.twi, A.ar, A.ninv);
+#pragma unroll
+            for (int t = 0; t < G::E; ++t) {
+                const uint32_t gi = ti + cbrv(t, G::LOGE) * T;
+                const uint64_t a = acc[gi];
+                acc[gi] = addq((uint64_t)A.ar.red1q(oacc[t]), canon ? a : red_q(a, q, mu), q);
+            }
+        } else {
+            inv_poly_from_regs<K, kPfSingle, false>(lds, oacc, ti, nullptr, true, A, A.ninv, 0,
+                                                    [&](uint32_t gi, uint64_t x) -> uint64_t {
+                                                        const uint64_t a = acc[gi];
+                                                        acc[gi] = addq(x, canon ? a : red_q(a, q, mu), q);
+                                                        return 0;
+                                                    });
+        }
         __syncthreads();
         canon = true;
     }
