@@ -238,16 +238,18 @@ int fhe_ct_multiply_relin_batch(fhe_ctx *ctx, uint32_t base_log, uint32_t level,
  *   = lwe_dim prepared GGSWs ([lwe_dim][(k+1)*level][k+1][n]).  k = 1 with
  *   n <= 16384 runs fused: one launch for the whole loop at n = 512..4096
  *   (two CUs per ciphertext while 16 * ceil(batch / 8) <= CUs, else one;
- *   FHE_BR_PAIR=0 forces one), per-step CMux launches above; k = 2..4 run
+ *   2 * level CUs at level 2 / 3 while 2 * level * ceil(batch / 8) <= the
+ *   CUs of one XCD, FHE_BR_MULTI=0 keeps two; FHE_BR_PAIR=0 forces one),
+ *   per-step CMux launches above; k = 2..4 run
  *   as one launch where the k + 1 accumulators fit in LDS (n = 512 / 1024
  *   with 64-bit words; n = 2048 for k <= 3 with 32-bit words); other
  *   k <= 16 and n = 32768 / 65536 run composed step by step (one digit
- *   buffer for the whole loop, stream-ordered, no host synchronisation).  The two-CU launch
- *   needs its workgroup pairs co-resident.  It is a cooperative launch
- *   (grid checked against the device's occupancy), pair launches of one
- *   process are serialised per device, and a workgroup whose partner does
- *   not answer within FHE_BR_PAIR_TIMEOUT_US (default 20000 us; 0 simulates
- *   a partner that never answers, for tests) gives its
+ *   buffer for the whole loop, stream-ordered, no host synchronisation).  The multi-CU
+ *   launch needs the workgroups of a ciphertext co-resident.  It is never
+ *   assumed: multi-CU launches of one process are serialised per device,
+ *   and a workgroup whose partners do not answer within
+ *   FHE_BR_PAIR_TIMEOUT_US (default 20000 us; 0 simulates a partner that
+ *   never answers, for tests) gives its
  *   ciphertext up: a repair pass enqueued behind the launch recomputes every
  *   given-up ciphertext on one CU from a saved copy of its input, so the
  *   result is exact in every case (no host synchronisation either way).
@@ -266,7 +268,7 @@ int fhe_blind_rotate_batch(fhe_ctx *ctx, uint32_t k, uint32_t base_log, uint32_t
                            uint64_t *acc, size_t batch, int where);
 int fhe_sample_extract_batch(fhe_ctx *ctx, uint32_t k, const uint64_t *glwe, uint64_t *lwe_a, uint64_t *lwe_b,
                              size_t batch, int where);
-/* Ciphertexts of this context's two-CU blind rotations that were recomputed
+/* Ciphertexts of this context's multi-CU blind rotations that were recomputed
  * by the repair pass since the context was created (a partner workgroup that
  * was not co-resident in time; see fhe_blind_rotate_batch).  Waits for the
  * context's stream.  No reference counterpart: blind_rotate
