@@ -408,3 +408,24 @@ def test_key_switch_rejects_entry_count_overflow():
     # the limit itself is fine for the shape check (batch 0: nothing to run)
     assert lib.fhe_key_switch_batch(P27, 4, 2, (1 << 31) - 1, 16, None, None, None, None, None, None, 0, 1, 0,
                                     None) == 0
+
+
+def test_cpu_calibration_record():
+    """bench.py's cpu_baseline.calibration: the committed
+    tools/calibrate_cpu.py run, per config port time / compiled-reference
+    time, and the later rerun carried beside it."""
+    import json
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    cal = bench.cpu_calibration(16384, 132120577)
+    raw = json.load(open(os.path.join(ROOT, "profiles", "r6_cpu_calibration.json")))
+    assert cal["ratio_median_all_configs"] == raw["ratio_median"]
+    fw = cal["forward_ntt_N16384"]
+    assert fw["reference_us"] == 2843.0 and abs(fw["ratio"] - fw["port_us"] / 2843.0) < 1e-12
+    assert cal["multiply_N16384"]["reference_us"] == 8603.0
+    assert cal["within_10pct_at_this_config"] == (0.9 <= fw["ratio"] <= 1.1)
+    assert len(raw["rows"]) == 12 and all(r["ratio"] == r["port_us"] / r["reference_us"] for r in raw["rows"])
+    assert "rerun" in cal and cal["rerun"]["ratio_range"][0] <= cal["rerun"]["ratio_median_all_configs"]
